@@ -1,0 +1,283 @@
+"""hiphuff -- MI355X-native parallel Huffman decoder (Python host binding).
+
+A thin ctypes layer over the C ABI in ``include/hiphuff.h`` (the library
+``libhiphuff.so`` in this package directory, built by the top-level
+Makefile).  The decode itself always runs in the HIP kernels; there is no CPU
+fallback in this package -- if the library (or a GPU) is missing, the calls
+raise.
+
+Mirrors the reference's plugin interface (framework/decodeUtil.h:14-19): a
+``Decoder`` is the device state behind one decoder function, ``decode_host``
+is the evaluate()-timed scope (H2D + decode + D2H, decodeUtil.c:41-43) and
+``decode_device`` is the HBM-resident hot path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhiphuff.so")
+PAYLOAD_PAD = 64   # HH_PAYLOAD_PAD
+
+_ERRORS = {
+    0: "ok", -1: "bad argument", -2: "i/o error", -3: "not a HUFF/HUFX file",
+    -4: "invalid code tree", -5: "output buffer too small", -6: "HIP runtime error",
+    -7: "out of memory", -8: "internal error", -9: "in-kernel wait timed out",
+    -10: "unsupported input",
+}
+
+
+class HipHuffError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        super().__init__(f"{what}: {_ERRORS.get(status, status)} ({status})")
+
+
+class _Huff(C.Structure):
+    _fields_ = [("nodes", C.c_int32), ("izero", C.POINTER(C.c_int32)),
+                ("ione", C.POINTER(C.c_int32)), ("sym", C.POINTER(C.c_uint8)),
+                ("bits", C.c_uint64), ("uncompressedsize", C.c_uint64),
+                ("data", C.POINTER(C.c_uint8)), ("wide", C.c_int)]
+
+
+class _Tree(C.Structure):
+    _fields_ = [("nodes", C.c_int32), ("izero", C.c_void_p), ("ione", C.c_void_p),
+                ("sym", C.c_void_p)]
+
+
+class _TreeInfo(C.Structure):
+    _fields_ = [("reachable", C.c_int32), ("leaves", C.c_int32), ("minlen", C.c_int32),
+                ("maxlen", C.c_int32), ("len_gcd", C.c_int32)]
+
+
+class _Config(C.Structure):
+    _fields_ = [("device", C.c_int), ("lane_bits", C.c_int), ("flags", C.c_int)]
+
+
+class _Stats(C.Structure):
+    _fields_ = [("ms_total", C.c_double), ("ms_sync", C.c_double), ("ms_scan", C.c_double),
+                ("ms_emit", C.c_double), ("out_len", C.c_uint64), ("lanes", C.c_uint64),
+                ("repairs", C.c_uint64), ("exact_fallback", C.c_int)]
+
+
+FLAG_FORCE_EXACT = 1
+_lib_handle: Optional[C.CDLL] = None
+
+# exported symbols and their ctypes signatures; tests check every one of these
+# against include/hiphuff.h
+_SIGS = {
+    "hh_strerror": ([C.c_int], C.c_char_p),
+    "hh_tree_check": ([C.POINTER(_Tree), C.POINTER(_TreeInfo)], C.c_int),
+    "hh_huff_load": ([C.c_char_p, C.POINTER(_Huff)], C.c_int),
+    "hh_huff_save": ([C.c_char_p, C.POINTER(_Huff)], C.c_int),
+    "hh_huff_free": ([C.POINTER(_Huff)], None),
+    "hh_huff_tree": ([C.POINTER(_Huff)], _Tree),
+    "hh_encode_bound": ([C.POINTER(_Tree), C.c_uint64], C.c_uint64),
+    "hh_encode": ([C.POINTER(_Tree), C.c_void_p, C.c_uint64, C.c_void_p,
+                   C.POINTER(C.c_uint64)], C.c_int),
+    "hh_decoder_create": ([C.POINTER(C.c_void_p), C.POINTER(_Config)], C.c_int),
+    "hh_decoder_destroy": ([C.c_void_p], None),
+    "hh_decoder_set_tree": ([C.c_void_p, C.POINTER(_Tree)], C.c_int),
+    "hh_decoder_stats": ([C.c_void_p, C.POINTER(_Stats)], C.c_int),
+    "hh_decode_device": ([C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                          C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
+    "hh_decode_host": ([C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                        C.POINTER(C.c_uint64)], C.c_int),
+    "hh_stage_initbitsindex": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p], C.c_int),
+    "hh_stage_decodeallbits": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                C.c_void_p], C.c_int),
+    "hh_stage_makebigtable": ([C.c_void_p, C.c_int64, C.c_void_p, C.c_int32,
+                               C.POINTER(C.c_int32), C.c_void_p], C.c_int),
+    "hh_stage_calcbitsindex": ([C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32,
+                                C.c_int32, C.c_void_p], C.c_int),
+    "hh_stage_calcresult": ([C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                             C.c_void_p], C.c_int),
+    "hh_stage_findmax": ([C.c_void_p, C.c_int64, C.c_void_p, C.POINTER(C.c_int32),
+                          C.c_void_p], C.c_int),
+    "hh_stage_pipeline": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint64,
+                           C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
+    "hipHuffApproach": ([C.c_void_p, C.c_void_p, C.c_void_p], None),
+}
+
+
+def lib() -> C.CDLL:
+    """The HIP library; raises if it was not built (no silent fallback)."""
+    global _lib_handle
+    if _lib_handle is None:
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7.
+        # Loading torch first lets libhiphuff.so bind to that same runtime
+        # (same soname), so device pointers and streams are shared with torch.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (args, res) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib_handle = L
+    return _lib_handle
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise HipHuffError(rc, what)
+
+
+@dataclass
+class HuffFile:
+    """A .huff container (HUFF or 64-bit HUFX), huffdata.c:27-68."""
+    izero: np.ndarray
+    ione: np.ndarray
+    sym: np.ndarray
+    bits: int
+    uncompressedsize: int
+    data: np.ndarray       # payload + PAYLOAD_PAD zero bytes
+
+    @property
+    def nodes(self) -> int:
+        return int(self.izero.shape[0])
+
+    @property
+    def payload(self) -> np.ndarray:
+        return self.data[: (self.bits + 7) // 8]
+
+    @classmethod
+    def load(cls, path: str) -> "HuffFile":
+        h = _Huff()
+        _check(lib().hh_huff_load(path.encode(), C.byref(h)), f"load {path}")
+        try:
+            n = h.nodes
+            iz = np.ctypeslib.as_array(h.izero, shape=(n,)).copy()
+            io = np.ctypeslib.as_array(h.ione, shape=(n,)).copy()
+            sy = np.ctypeslib.as_array(h.sym, shape=(n,)).copy()
+            nb = (h.bits + 7) // 8 + PAYLOAD_PAD
+            data = np.ctypeslib.as_array(h.data, shape=(nb,)).copy()
+            return cls(iz, io, sy, int(h.bits), int(h.uncompressedsize), data)
+        finally:
+            lib().hh_huff_free(C.byref(h))
+
+    def save(self, path: str, wide: bool = False):
+        keep = [np.ascontiguousarray(self.izero, np.int32),
+                np.ascontiguousarray(self.ione, np.int32),
+                np.ascontiguousarray(self.sym, np.uint8),
+                np.ascontiguousarray(self.data, np.uint8)]
+        h = _Huff(self.nodes, keep[0].ctypes.data_as(C.POINTER(C.c_int32)),
+                  keep[1].ctypes.data_as(C.POINTER(C.c_int32)),
+                  keep[2].ctypes.data_as(C.POINTER(C.c_uint8)), self.bits,
+                  self.uncompressedsize, keep[3].ctypes.data_as(C.POINTER(C.c_uint8)),
+                  int(wide))
+        _check(lib().hh_huff_save(path.encode(), C.byref(h)), f"save {path}")
+
+    def tree(self) -> "Tree":
+        return Tree(self.izero, self.ione, self.sym)
+
+
+class Tree:
+    """Code tree in the reference's node layout (huffdata.h:12-16), SoA."""
+
+    def __init__(self, izero, ione, sym):
+        self.izero = np.ascontiguousarray(izero, np.int32)
+        self.ione = np.ascontiguousarray(ione, np.int32)
+        self.sym = np.ascontiguousarray(sym, np.uint8)
+        self._c = _Tree(len(self.izero), self.izero.ctypes.data, self.ione.ctypes.data,
+                        self.sym.ctypes.data)
+
+    def info(self) -> dict:
+        inf = _TreeInfo()
+        _check(lib().hh_tree_check(C.byref(self._c), C.byref(inf)), "tree check")
+        return {k: getattr(inf, k) for k, _ in _TreeInfo._fields_}
+
+    def encode(self, syms: np.ndarray) -> tuple[np.ndarray, int]:
+        """Pack symbols LSB-first with this tree's codes -> (payload+pad, bits)."""
+        syms = np.ascontiguousarray(syms, np.uint8)
+        bound = lib().hh_encode_bound(C.byref(self._c), len(syms))
+        if bound == 0:
+            raise HipHuffError(-4, "encode bound")
+        out = np.zeros(bound + PAYLOAD_PAD, np.uint8)
+        bits = C.c_uint64(0)
+        _check(lib().hh_encode(C.byref(self._c), syms.ctypes.data, len(syms), out.ctypes.data,
+                               C.byref(bits)), "encode")
+        nb = (bits.value + 7) // 8
+        return out[: nb + PAYLOAD_PAD].copy(), int(bits.value)
+
+
+class Decoder:
+    """Device decoder: tables + workspace on one GPU (hh_decoder_*)."""
+
+    def __init__(self, device: int = 0, lane_bits: int = 0, flags: int = 0):
+        self._h = C.c_void_p()
+        cfg = _Config(device, lane_bits, flags)
+        _check(lib().hh_decoder_create(C.byref(self._h), C.byref(cfg)), "decoder create")
+        self.device = device
+        self._tree = None
+
+    def close(self):
+        if self._h:
+            lib().hh_decoder_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_tree(self, tree: Tree):
+        _check(lib().hh_decoder_set_tree(self._h, C.byref(tree._c)), "set tree")
+        self._tree = tree
+
+    def stats(self) -> dict:
+        st = _Stats()
+        _check(lib().hh_decoder_stats(self._h, C.byref(st)), "stats")
+        return {k: getattr(st, k) for k, _ in _Stats._fields_}
+
+    def decode_host(self, payload: np.ndarray, bits: int, cap: int) -> np.ndarray:
+        payload = np.ascontiguousarray(payload, np.uint8)
+        out = np.zeros(max(cap, 1), np.uint8)
+        n = C.c_uint64(0)
+        _check(lib().hh_decode_host(self._h, payload.ctypes.data, bits, out.ctypes.data, cap,
+                                    C.byref(n)), "decode_host")
+        return out[: n.value]
+
+    def decode_device_ptr(self, d_data: int, bits: int, d_out: int, cap: int,
+                          stream: int = 0) -> int:
+        n = C.c_uint64(0)
+        _check(lib().hh_decode_device(self._h, d_data, bits, d_out, cap, C.byref(n),
+                                      stream or None), "decode_device")
+        return int(n.value)
+
+    def decode_device(self, data, bits: int, out, stream=None) -> int:
+        """Decode torch uint8 CUDA tensors (data holds payload + pad)."""
+        import torch
+        assert data.is_cuda and out.is_cuda and data.dtype == torch.uint8
+        assert data.numel() >= (bits + 7) // 8 + PAYLOAD_PAD
+        s = stream if stream is not None else torch.cuda.current_stream(data.device)
+        return self.decode_device_ptr(data.data_ptr(), bits, out.data_ptr(), out.numel(),
+                                      s.cuda_stream)
+
+    def stage_pipeline_ptr(self, d_data: int, bits: int, d_out: int, cap: int,
+                           stream: int = 0) -> int:
+        n = C.c_uint64(0)
+        _check(lib().hh_stage_pipeline(self._h, d_data, bits, d_out, cap, C.byref(n),
+                                       stream or None), "stage_pipeline")
+        return int(n.value)
+
+
+def decode_file(path: str, device: int = 0) -> np.ndarray:
+    """Load a .huff and decode it on the GPU (host-to-host)."""
+    hf = HuffFile.load(path)
+    dec = Decoder(device)
+    try:
+        dec.set_tree(hf.tree())
+        return dec.decode_host(hf.payload, hf.bits, hf.bits + 1)
+    finally:
+        dec.close()

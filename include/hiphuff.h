@@ -1,0 +1,201 @@
+/*
+ * hiphuff.h -- C ABI of the MI355X-native parallel Huffman decoder.
+ *
+ * Plain C types only (pointers, sizes, status codes): this is the drop-in
+ * boundary a host program links against (libhiphuff.so).  Each entry point
+ * names the reference interface it replaces (BeauJoh/HuffmanDecoderOnGPUs,
+ * paths relative to framework/).
+ *
+ * Layering
+ *   hh_huff_*      .huff container (HUFF + 64-bit HUFX)     replaces huffdata.c:27-68
+ *   hh_decoder_*   device decoder state (tables, workspace)  replaces the lazy CL/CUDA
+ *                                                             globals, openclapproach.c:231-234
+ *   hh_decode_*    the hot path                               replaces openclApproach
+ *                                                             (openclapproach.c:236-1047) and
+ *                                                             fastgpuApproach (fastgpu.cu:140-332)
+ *   hh_stage_*     reference-shaped stage kernels             replaces the six kernels of
+ *                                                             ReleaseCL/kernels/ *.cl one by one
+ *   hipHuffApproach  plugin with the reference's decoder       decodeUtil.h:14-19 function-pointer
+ *                    signature (see hiphuff_plugin.h)          type, registered like mainrun.c:480-488
+ *
+ * Every function returns HH_OK (0) or a negative hh_status; nothing aborts
+ * the process (the plugin wrapper converts errors to the reference's
+ * exit(1) behaviour, decodeUtil.c:47-52).
+ */
+#ifndef HIPHUFF_H_
+#define HIPHUFF_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HIPHUFF_VERSION_MAJOR 0
+#define HIPHUFF_VERSION_MINOR 1
+
+typedef enum {
+    HH_OK = 0,
+    HH_ERR_ARG = -1,          /* bad argument (null pointer, size)            */
+    HH_ERR_IO = -2,           /* file could not be opened / read / written    */
+    HH_ERR_FORMAT = -3,       /* not a HUFF/HUFX container, truncated         */
+    HH_ERR_TREE = -4,         /* tree is not a proper binary tree from node 0,
+                                 or the root is a leaf (the reference loops
+                                 forever on such a tree, pes.c:151-161)       */
+    HH_ERR_CAPACITY = -5,     /* output buffer too small for the decode       */
+    HH_ERR_DEVICE = -6,       /* HIP runtime error                            */
+    HH_ERR_NOMEM = -7,        /* host or device allocation failed             */
+    HH_ERR_INTERNAL = -8,     /* internal consistency check failed            */
+    HH_ERR_TIMEOUT = -9,      /* bounded in-kernel wait expired               */
+    HH_ERR_UNSUPPORTED = -10  /* input outside what this entry point handles  */
+} hh_status;
+
+const char *hh_strerror(int status);
+
+/* ---------------------------------------------------------------------- */
+/* Code tree.  Same information as struct HuffNode (huffdata.h:12-16):    */
+/* node 0 is the root, a leaf has izero == ione == -1, bit 0 follows      */
+/* izero, bit 1 follows ione.  Structure-of-arrays, no padding games.     */
+/* ---------------------------------------------------------------------- */
+typedef struct {
+    int32_t nodes;
+    const int32_t *izero;
+    const int32_t *ione;
+    const uint8_t *sym;
+} hh_tree;
+
+/* Static facts about a tree (validated: reachable part is a full binary
+ * tree rooted at 0, no cycles). */
+typedef struct {
+    int32_t reachable;   /* nodes reachable from the root                 */
+    int32_t leaves;      /* reachable leaves                              */
+    int32_t minlen;      /* shortest code (tableMinDepth, huffdata.c:272) */
+    int32_t maxlen;      /* longest code  (tableHeight,  huffdata.c:224)  */
+    int32_t len_gcd;     /* gcd of all code lengths                       */
+} hh_tree_info;
+
+int hh_tree_check(const hh_tree *tree, hh_tree_info *info);
+
+/* ---------------------------------------------------------------------- */
+/* Container: loadHuffFile (huffdata.c:27-68) with 64-bit sizes.          */
+/*   "HUFF": be-i32 nodes, be-i32 bits, be-i32 uncompressedsize,          */
+/*           nodes x {u8 sym, be-i32 izero, be-i32 ione}, ceil(bits/8) B  */
+/*   "HUFX": be-i32 nodes, be-i64 bits, be-i64 uncompressedsize, then the */
+/*           same tree and payload (the 64-bit sibling for > 2^31 bits).  */
+/* The loaded payload is followed by HH_PAYLOAD_PAD zero bytes.           */
+/* ---------------------------------------------------------------------- */
+#define HH_PAYLOAD_PAD 64
+
+typedef struct {
+    int32_t nodes;
+    int32_t *izero;
+    int32_t *ione;
+    uint8_t *sym;
+    uint64_t bits;
+    uint64_t uncompressedsize;
+    uint8_t *data;           /* ceil(bits/8) + HH_PAYLOAD_PAD bytes       */
+    int wide;                /* 1 if read from / to be written as HUFX    */
+} hh_huff;
+
+int hh_huff_load(const char *path, hh_huff *out);
+/* Writes HUFF when bits and size fit int32 (and !h->wide), else HUFX.    */
+int hh_huff_save(const char *path, const hh_huff *h);
+void hh_huff_free(hh_huff *h);
+hh_tree hh_huff_tree(const hh_huff *h);
+
+/* ---------------------------------------------------------------------- */
+/* Encoder (the reference ships none).  Builds the    */
+/* canonical bit strings of `tree` and packs `n` symbols LSB-first.       */
+/* out must hold hh_encode_bound(tree, n) bytes; *bits gets the length.   */
+/* Symbols absent from the tree are an HH_ERR_ARG.                        */
+/* ---------------------------------------------------------------------- */
+uint64_t hh_encode_bound(const hh_tree *tree, uint64_t n);
+int hh_encode(const hh_tree *tree, const uint8_t *syms, uint64_t n,
+              uint8_t *out, uint64_t *bits);
+
+/* ---------------------------------------------------------------------- */
+/* Device decoder.                                                        */
+/* ---------------------------------------------------------------------- */
+typedef struct hh_decoder hh_decoder;
+
+typedef struct {
+    int device;              /* HIP device ordinal                           */
+    int lane_bits;           /* bits per lane region, 0 = default            */
+    int flags;               /* HH_FLAG_*                                    */
+} hh_config;
+
+#define HH_FLAG_FORCE_EXACT 1   /* skip the sync fast path, use the exact
+                                   transfer-function path throughout */
+
+int hh_decoder_create(hh_decoder **dec, const hh_config *cfg);
+void hh_decoder_destroy(hh_decoder *dec);
+
+/* Upload / replace the code tree (builds the lookup tables on the host,
+ * copies them to the device).  The tree may be reused across decodes. */
+int hh_decoder_set_tree(hh_decoder *dec, const hh_tree *tree);
+
+/* Statistics of the last decode (device time of each phase, in ms). */
+typedef struct {
+    double ms_total;         /* hipEvent time of the whole device pipeline  */
+    double ms_sync;          /* speculative decode + chain stitching        */
+    double ms_scan;          /* offsets                                      */
+    double ms_emit;          /* symbol emission                              */
+    uint64_t out_len;        /* symbols decoded                              */
+    uint64_t lanes;          /* lane regions                                 */
+    uint64_t repairs;        /* lane walks that needed a repair              */
+    int exact_fallback;      /* 1 if the transfer-function path was used    */
+} hh_stats;
+
+int hh_decoder_stats(const hh_decoder *dec, hh_stats *st);
+
+/* Decode `bits` bits at device pointer d_data (it must be readable for
+ * ceil(bits/8) + HH_PAYLOAD_PAD bytes; the pad content is ignored) into
+ * device buffer d_out (cap bytes).  *out_len receives the number of
+ * symbols, i.e. the length the reference computes with findmax + 1
+ * (findmax.cl:2-8).  Enqueued on `hip_stream` (a hipStream_t, NULL = the
+ * default stream); the call returns after the output length is known.    */
+int hh_decode_device(hh_decoder *dec, const void *d_data, uint64_t bits,
+                     void *d_out, uint64_t cap, uint64_t *out_len,
+                     void *hip_stream);
+
+/* Host-to-host convenience: H2D, hh_decode_device, D2H.  This is the scope
+ * the reference times in evaluate() (decodeUtil.c:41-43). */
+int hh_decode_host(hh_decoder *dec, const uint8_t *data, uint64_t bits,
+                   uint8_t *out, uint64_t cap, uint64_t *out_len);
+
+/* ---------------------------------------------------------------------- */
+/* Reference-shaped stage kernels (one HIP kernel per reference kernel,   */
+/* int32 arrays exactly as pes.c / the .cl kernels lay them out).  For    */
+/* parity of intermediate arrays; O(25 * bits) memory, bits < 2^31.       */
+/* All pointers are device pointers.                                      */
+/* ---------------------------------------------------------------------- */
+/* initbitsindex.cl:4-12 */
+int hh_stage_initbitsindex(hh_decoder *dec, int32_t *d_bitsindex, int64_t bits,
+                           void *hip_stream);
+/* decodeallbits.cl:10-33: sym per bit, level-0 lengths into d_steps[0..bits) */
+int hh_stage_decodeallbits(hh_decoder *dec, const void *d_data, int64_t bits,
+                           uint8_t *d_bitdecode, int32_t *d_steps, void *hip_stream);
+/* makebigtable.cl:10-40: level `step` -> step+1; *flag gets steps[step][0] */
+int hh_stage_makebigtable(hh_decoder *dec, int64_t bits, int32_t *d_steps,
+                          int32_t step, int32_t *flag, void *hip_stream);
+/* calcbitsindex.cl:5-22 */
+int hh_stage_calcbitsindex(hh_decoder *dec, int64_t bits, int32_t *d_bitsindex,
+                           const int32_t *d_steps, int32_t step, int32_t powertwo,
+                           void *hip_stream);
+/* calcresult.cl:5-19 */
+int hh_stage_calcresult(hh_decoder *dec, int64_t bits, const int32_t *d_bitsindex,
+                        const uint8_t *d_bitdecode, uint8_t *d_result,
+                        void *hip_stream);
+/* findmax.cl:2-8 (parallel max-reduction instead of one work-item) */
+int hh_stage_findmax(hh_decoder *dec, int64_t bits, const int32_t *d_bitsindex,
+                     int32_t *maxvalue, void *hip_stream);
+/* The six stages driven like openclApproach; returns the output length. */
+int hh_stage_pipeline(hh_decoder *dec, const void *d_data, int64_t bits,
+                      uint8_t *d_out, uint64_t cap, uint64_t *out_len,
+                      void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

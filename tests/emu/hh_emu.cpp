@@ -1,0 +1,116 @@
+// hh_emu.cpp -- TEST-ONLY host emulation of the fast-path kernels.
+//
+// Runs the same per-lane building blocks as the HIP kernels (hh_algo.h) on
+// host arrays, tile by tile, lane by lane, so the stitching logic can be
+// checked against the oracle on machines without a GPU.  Nothing in the
+// product links this file; it builds into tests/emu/libhh_emu.so.
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "hh_algo.h"
+#include "hiphuff.h"
+
+extern "C" {
+
+// stats[0]=tiles stats[1]=walks with k>1 stats[2]=failed walks
+// stats[3]=max k seen
+int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *sym,
+                      int32_t nodes, const uint8_t *data, uint64_t bits, uint32_t S,
+                      uint8_t *out, uint64_t cap, int64_t *stats) {
+    hh_tree tree = {nodes, izero, ione, sym};
+    static hh_tables T;   // large; not reentrant (test helper)
+    int rc = hh_tables_build(&tree, &T);
+    if (rc) return rc;
+    for (int i = 0; i < 4; i++) stats[i] = 0;
+    if (bits == 0) return 0;
+    const uint64_t TB = (uint64_t)HH_NL * S;
+    const uint64_t ntiles = (bits + TB - 1) / TB;
+    const uint64_t nbytes = (bits + 7) / 8;
+    const uint32_t span = (HH_NL + HH_KM + 1) * S + 320;  // bits a tile may touch
+    const uint32_t nw = span / 32 + 3;
+    std::vector<uint32_t> w(nw);
+    std::vector<uint64_t> rec((size_t)ntiles * HH_NL), tab((size_t)ntiles * HH_KM);
+    stats[0] = (int64_t)ntiles;
+
+    auto load_tile = [&](uint64_t t, hh_ctx &c) {
+        uint64_t b0 = t * TB;
+        uint64_t w0 = b0 >> 5;
+        for (uint32_t i = 0; i < nw; i++) {
+            uint64_t byte = (w0 + i) * 4;
+            uint32_t v = 0;
+            for (int k = 0; k < 4; k++)
+                if (byte + k < nbytes) v |= (uint32_t)data[byte + k] << (8 * k);
+            w[i] = v;
+        }
+        c.w = w.data();
+        c.sh = (uint32_t)(b0 & 31);
+        c.l1 = T.l1;
+        c.l2 = T.l2;
+        c.tree = T.tree;
+        c.tsym = T.tsym;
+        uint64_t rem = bits - b0;
+        c.bt = rem < span ? (uint32_t)rem : span;
+    };
+
+    // K1: per lane count + walk, per tile table
+    for (uint64_t t = 0; t < ntiles; t++) {
+        hh_ctx c;
+        load_tile(t, c);
+        for (uint32_t lane = 0; lane < HH_NL; lane++) {
+            uint32_t p0 = lane * S;
+            hh_rec r;
+            uint32_t n = 0, x = p0;
+            if (p0 < c.bt) x = hh_region_count(&c, p0, p0 + S, &n);
+            hh_walk(&c, lane, S, x, &r);
+            r.n = n;
+            if (r.k == 0) stats[2]++;
+            if (r.k > 1) stats[1]++;
+            if ((int64_t)r.k > stats[3]) stats[3] = r.k;
+            rec[t * HH_NL + lane] = hh_rec_pack(r);
+        }
+        hh_tile_table_seq(&rec[t * HH_NL], &tab[t * HH_KM]);
+    }
+    if (stats[2]) return HH_ERR_UNSUPPORTED;
+
+    // K2: scan over tile tables
+    std::vector<hh_state> st(ntiles + 1);
+    st[0] = hh_state{0, 0, 0, 0};
+    for (uint64_t t = 0; t < ntiles; t++) st[t + 1] = hh_xf_apply(&tab[t * HH_KM], st[t]);
+    uint64_t total = st[ntiles].base;
+    if (total > cap) return HH_ERR_CAPACITY;
+
+    // K3: emission
+    struct Sink {
+        uint8_t *out;
+        void operator()(uint64_t o, uint32_t b) { out[o] = (uint8_t)b; }
+    } sink{out};
+    for (uint64_t t = 0; t < ntiles; t++) {
+        hh_ctx c;
+        load_tile(t, c);
+        hh_state s = st[t];
+        uint32_t j = s.d, e_in = s.e;
+        int32_t del_in = s.delta;
+        uint64_t o = s.base;
+        while (j < HH_NL) {
+            hh_rec r = hh_rec_unpack(rec[t * HH_NL + j]);
+            uint32_t nx = hh_rec_next(j, r);
+            uint32_t start = j * S + e_in, end = nx * S + r.e;
+            uint32_t pe = end < c.bt ? end : c.bt;
+            uint64_t cnt = (uint64_t)((int64_t)r.n + r.cov + del_in);
+            uint32_t p = start;
+            uint64_t o0 = o;
+            if (p < pe) hh_emit_run(&c, &p, pe, &o, total, sink);
+            if (o - o0 != cnt) return HH_ERR_INTERNAL;   // count/emission disagree
+            e_in = r.e;
+            del_in = r.delta;
+            j = nx;
+        }
+        if (o != st[t + 1].base) return HH_ERR_INTERNAL;
+    }
+    return (int64_t)total;
+}
+
+}  // extern "C"
