@@ -14,7 +14,7 @@ CSRC     := $(PKG)/csrc
 BUILD    := build
 INC      := -Iinclude -I$(CSRC)
 CFLAGS   := -O3 -fPIC -Wall -Wextra -std=gnu11 $(INC)
-HIPFLAGS := -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-result -Wno-unused-value \
+HIPFLAGS := $(HIPEXTRA) -O3 -fPIC -std=c++17 --offload-arch=$(ARCH) -Wall -Wno-unused-result -Wno-unused-value \
             -Wno-comment $(INC)
 
 LIB      := $(PKG)/libhiphuff.so
@@ -57,3 +57,9 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all lib cli emu oracle clean
+
+# diagnostic build: per-phase s_memtime stamps (tools/diag_stamps.py)
+stamps: $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
+	$(HIPCC) -DHH_STAMPS $(HIPFLAGS) -c $(CSRC)/hh_device.hip -o $(BUILD)/hh_device_stamps.o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/libhiphuff_stamps.so $(BUILD)/hh_device_stamps.o $^
+.PHONY: stamps

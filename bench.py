@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""bench.py -- decoded MB/s and HBM roofline fraction of the HIP decoder.
+
+Workload (BASELINE.json configs[2]): a synthetic 1 GiB English-text .huff --
+kjv.txt tiled (about 349.4 copies) and encoded with the files/kjv.txt.huff
+codebook, cut at a symbol boundary -- decoded on each MI355X.  One "step" is
+one full decode of that stream with the input already resident in HBM:
+hh_decode_device (k_sync + k_scan + k_emit) plus its 16-byte status
+readback.  For N > 1 the stream is N GiB, sharded by byte ranges (weak
+scaling); the shards exchange transfer tables (a tiny all-gather) before
+decoding, and the decoded segments are all-gathered once after the timed
+region (reported separately).
+
+Prints ONE JSON line on rank 0.  `roofline` is computed from the device-event
+duration of the decode (C + D algorithmic bytes per decode); `cpu_baseline`
+times the reference's own linApproach (oracle/_ref, compiled from the
+reference's C sources) or, if that was not built, the oracle's restatement,
+on a bounded sample (kjv.txt.huff) on one host core.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size-mib", type=int, default=1024, help="compressed MiB per GPU")
+    ap.add_argument("--files", default=os.path.join(ROOT, "files"))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
+                    help="HBM traffic measured by rocprofv3 --pmc (tools/profile.sh)")
+    return ap.parse_args()
+
+
+def cpu_baseline(files_dir: str, seconds: float) -> dict:
+    """linApproach on kjv.txt.huff, one core: sweep jumpbits 1..14 once
+    (the reference's testall sweep, mainrun.c:456-459), then repeat the best
+    for ~`seconds`; report decoded MB/s of the median repeat."""
+    from oracle import oracle as O
+    path = os.path.join(files_dir, "kjv.txt.huff")
+    if O.ref_available():
+        kind = "reference"
+        h = O.RefHuff(path)
+        run = lambda J: h.run("linApproach", J)          # noqa: E731
+        D = h.uncompressedsize
+    else:
+        kind = "port"
+        h = O.OracleHuff.load(path)
+        run = h.lin_decode                                 # noqa: E731
+        D = h.uncompressedsize
+    best_j, best_t = None, None
+    for J in range(1, 15):
+        t0 = time.perf_counter()
+        run(J)
+        t = time.perf_counter() - t0
+        if best_t is None or t < best_t:
+            best_j, best_t = J, t
+    times = []
+    t_end = time.perf_counter() + seconds
+    while time.perf_counter() < t_end or len(times) < 3:
+        t0 = time.perf_counter()
+        run(best_j)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    cpu = platform.processor() or "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": round(D / med / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": kind,
+            "sample": (f"linApproach(jumpbits={best_j}) on files/kjv.txt.huff "
+                       f"({D} B decoded), median of {len(times)} runs over ~{seconds:.0f} s, "
+                       f"tables built inside each timed call; host {cpu}, "
+                       f"nproc {os.cpu_count()}")}
+
+
+def load_pmc(path: str, workload: str):
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_decode")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    a = _args()
+    import torch
+    import torch.distributed as dist
+    import huffmandecoderongpus_amd as H
+    from huffmandecoderongpus_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    hf, text = synth.load_source(a.files, "kjv.txt", device=local)
+    target = a.size_mib << 20
+    if world > 1:
+        from huffmandecoderongpus_amd import shard as SH
+        job = SH.ShardJob(hf, text, target, rank, world, local)
+        run_step = job.decode_step
+        C_bytes, D_bytes = job.compressed_bytes, job.decoded_bytes
+        dec = job.dec
+    else:
+        syn = synth.tiled_stream(hf, text, target, device=dev)
+        dec = H.Decoder(local)
+        dec.set_tree(syn.tree)
+        out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device=dev)
+        stream = torch.cuda.current_stream(dev)
+        C_bytes, D_bytes = syn.compressed_bytes, syn.decoded_bytes
+
+        def run_step():
+            return dec.decode_device(syn.data, syn.bits, out, stream)
+
+    # correctness of the measured configuration, outside the timed region
+    n = run_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        ok = job.verify()
+    else:
+        ok = n == syn.decoded_bytes and synth.verify_tiled(out, syn)
+    if not ok:
+        raise SystemExit(f"rank {rank}: decoded output does not match the tiled text")
+
+    for _ in range(a.warmup):
+        run_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dev_ms = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        run_step()
+        dev_ms.append(dec.stats())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_step = elapsed / a.steps * 1e3
+    ms_dev = statistics.mean(s["ms_total"] for s in dev_ms)
+    kern = {k: round(statistics.mean(s[k] for s in dev_ms), 4)
+            for k in ("ms_sync", "ms_scan", "ms_emit")}
+    extra = {}
+    if world > 1:
+        extra = job.gather_report()
+        tot = torch.tensor([C_bytes, D_bytes], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+        C_all, D_all = int(tot[0].item()), int(tot[1].item())
+    else:
+        C_all, D_all = C_bytes, D_bytes
+    workload = f"synthetic {a.size_mib} MiB/GPU kjv-tiled .huff"
+    achieved = (C_bytes + D_bytes) / (ms_dev * 1e-3) / 1e9
+    traffic = load_pmc(a.pmc, workload)
+    res = {
+        "metric": "decoded MB/s",
+        "value": round(D_all / (ms_step * 1e-3) / 1e6, 1),
+        "unit": "MB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": ("synthetic: files/kjv.txt tiled and encoded with the kjv.txt.huff "
+                 "codebook (payload bit-concatenation), cut at a symbol boundary"),
+        "config": {"workload": workload + (f", sharded over {world} GPUs" if world > 1 else ", 1 MI355X"),
+                   "compressed_bytes": C_all, "decoded_bytes": D_all,
+                   "bits_per_gpu": int(C_bytes * 8), "parallelism": f"byte-range shards x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "decode pipeline k_sync+k_scan+k_emit",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "bytes_alg": C_bytes + D_bytes, "ms_device": round(ms_dev, 4),
+                     "ms_kernels": kern},
+        "decoded_MBps_device": round(D_bytes / (ms_dev * 1e-3) / 1e6, 1),
+    }
+    res.update(extra)
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(a.files, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

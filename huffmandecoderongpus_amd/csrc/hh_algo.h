@@ -240,6 +240,159 @@ HH_HD void hh_walk(const hh_ctx *c, uint32_t lane, uint32_t S, uint32_t x,
 }
 
 /* ------------------------------------------------------------------ */
+/* Boundary masks.  Phase A also records, for its region, a bit per     */
+/* position that starts a code of its offset-0 chain (mask word w, bit  */
+/* i <=> position 32w + i of the region).  A walk then decodes only the */
+/* incoming chain, several codes per lookup, and tests each lookup's    */
+/* start positions against the next region's mask -- the first common   */
+/* start is exactly the two-pointer merge point (hh_walk), found in a   */
+/* fraction of the steps.                                               */
+/* ------------------------------------------------------------------ */
+#define HH_MW_MAX 10   /* mask words per region (S <= 320) */
+
+typedef struct {
+    const uint32_t *m;    /* [nreg][mw] region masks            */
+    const uint16_t *x;    /* [nreg] exit offset from region start */
+    const uint16_t *n;    /* [nreg] own-chain symbol counts        */
+    uint32_t nreg;        /* regions with a mask (tile-local 0..)  */
+    uint32_t mw;          /* words per region mask                 */
+} hh_masks;
+
+/* Phase A with the boundary mask: like hh_region_count, plus
+ * sink(w, word) for every mask word w in [0, mw). */
+template <class MaskSink>
+HH_HD uint32_t hh_region_count_mask(const hh_ctx *c, uint32_t p0, uint32_t lim, uint32_t mw,
+                                    uint32_t *count, MaskSink &sink) {
+    uint32_t p = p0, n = 0, wdone = 0, mbase = p0;
+    uint64_t macc = 0;
+    if (lim > c->bt) lim = c->bt;
+    while (p < lim) {
+        uint32_t win = hh_read32(c, p);
+        uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
+        uint32_t ns = HH_L1_NSYM(e);
+        uint32_t l, bm = 1u;
+        if (ns) {
+            uint32_t nb = HH_L1_NBITS(e);
+            if (p + nb <= lim) {
+                l = nb;
+                bm = HH_L1_BMASK(e);
+            } else {
+                l = HH_L1_LEN0(e);
+                ns = 1;
+            }
+        } else {
+            uint32_t s;
+            l = hh_escape(c, p, win, e, &s);
+            ns = 1;
+        }
+        macc |= (uint64_t)bm << (p - mbase);
+        uint32_t rem = c->bt - p;
+        p += l < rem ? l : rem;
+        n += ns;
+        while (p - mbase >= 32 && wdone < mw) {
+            sink(wdone++, (uint32_t)macc);
+            macc >>= 32;
+            mbase += 32;
+        }
+    }
+    while (wdone < mw) {
+        sink(wdone++, (uint32_t)macc);
+        macc >>= 32;
+    }
+    *count = n;
+    return p;
+}
+
+/* Symbols of region r's own chain that start before region offset `off`. */
+HH_HD uint32_t hh_mask_rank(const hh_masks *mk, uint32_t r, uint32_t off) {
+    const uint32_t *m = mk->m + r * mk->mw;
+    uint32_t cnt = 0, w = 0;
+    for (; w < (off >> 5); w++) cnt += __builtin_popcount(m[w]);
+    if (off & 31u) cnt += __builtin_popcount(m[w] & ((1u << (off & 31u)) - 1u));
+    return cnt;
+}
+
+/* Phase B with masks: same result as hh_walk.  Regions >= mk->nreg (past
+ * the tile's masks) fall back to the two-pointer walk. */
+HH_HD void hh_walk_mask(const hh_ctx *c, const hh_masks *mk, uint32_t lane, uint32_t S,
+                        uint32_t x, hh_rec *r) {
+    r->k = 1; r->e = 0; r->delta = 0; r->cov = 0;
+    uint32_t A = x;
+    uint32_t R = lane + 1;
+    if (A < R * S) return;      /* stream ended inside this region */
+    for (uint32_t it = 0; it < HH_KM; it++, R++) {
+        const uint32_t Lr = R * S, Le = Lr + S;
+        const uint32_t eA = A - Lr;
+        uint32_t ca = 0;
+        if (R < mk->nreg) {
+            const uint32_t *m = mk->m + R * mk->mw;
+            const uint32_t lim = Le < c->bt ? Le : c->bt;
+            while (A < lim) {
+                uint32_t win = hh_read32(c, A);
+                uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
+                uint32_t ns = HH_L1_NSYM(e), l, bm = 1u;
+                if (ns && A + HH_L1_NBITS(e) <= lim) {
+                    l = HH_L1_NBITS(e);
+                    bm = HH_L1_BMASK(e);
+                } else {
+                    if (ns) {
+                        l = HH_L1_LEN0(e);
+                    } else {
+                        uint32_t s;
+                        l = hh_escape(c, A, win, e, &s);
+                    }
+                    ns = 1;
+                }
+                const uint32_t off = A - Lr, wi = off >> 5, sh = off & 31u;
+                uint64_t mm = (uint64_t)m[wi];
+                if (wi + 1 < mk->mw) mm |= (uint64_t)m[wi + 1] << 32;
+                const uint32_t hit = bm & (uint32_t)(mm >> sh);
+                if (hit) {
+                    const uint32_t t = (uint32_t)__builtin_ctz(hit);
+                    const uint32_t a = ca + (uint32_t)__builtin_popcount(bm & ((1u << t) - 1u));
+                    const uint32_t b = hh_mask_rank(mk, R, off + t);
+                    r->k = it + 1;
+                    r->e = eA;
+                    r->delta = (int32_t)a - (int32_t)b;
+                    return;
+                }
+                uint32_t rem = c->bt - A;
+                A += l < rem ? l : rem;
+                ca += ns;
+            }
+            /* both chains leave the region at the same point -> merged there */
+            if (A == Lr + mk->x[R] || A >= c->bt) {
+                r->k = it + 1;
+                r->e = eA;
+                r->delta = (int32_t)ca - (int32_t)mk->n[R];
+                return;
+            }
+        } else {
+            uint32_t B = Lr, cb = 0;
+            for (;;) {
+                if (A == B) {
+                    r->k = it + 1;
+                    r->e = eA;
+                    r->delta = (int32_t)ca - (int32_t)cb;
+                    return;
+                }
+                uint32_t ad = A >= Le, bd = B >= Le;
+                if (ad && bd) break;
+                if (!ad && (bd || A < B)) {
+                    A += hh_len1(c, A);
+                    ca++;
+                } else {
+                    B += hh_len1(c, B);
+                    cb++;
+                }
+            }
+        }
+        r->cov += ca;
+    }
+    r->k = 0;
+}
+
+/* ------------------------------------------------------------------ */
 /* Cross-tile state and tile transfer tables.                          */
 /* The state entering a tile: d = first live lane of the tile (lanes    */
 /* before it are covered by a walk from the previous tile), e = its     */

@@ -134,235 +134,446 @@ __device__ __forceinline__ TileGeom tile_geom(uint64_t tile, uint32_t S, uint64_
 }
 
 // ---------------------------------------------------------------------------
-// K1: speculative region decode + stitching walks + tile transfer table
+// The fused decoder: one persistent kernel, tiles dispensed in order.
+//
+// Per tile: (1) stage the tile's bits (+ halo) in LDS; (2) every lane
+// decodes its region from offset 0 and walks its exit into the next region
+// until the chains share a boundary; (3) the tile resolves its live lanes for
+// every entering state d and publishes its HH_KM-entry transfer table
+// (AGGREGATE); (4) decoupled look-back over predecessors' tables / inclusive
+// states yields this tile's entering state and output base, published as
+// INCLUSIVE; (5) live lanes re-decode their runs into an LDS window, written
+// out with 16-byte stores.  C is read once, D written once.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(HH_NL) void k_sync(const uint32_t *__restrict__ gdata, uint64_t bits,
-                                                uint64_t nwords_ok, uint32_t S, DevTab tab,
-                                                uint64_t *__restrict__ rec,
-                                                uint64_t *__restrict__ ttab, uint32_t *flags) {
-    __shared__ uint64_t s_l1[HH_L1_SIZE];
-    __shared__ uint32_t s_w[HH_NW_MAX];
-    __shared__ uint8_t s_mem[HH_NL];
-    __shared__ uint8_t s_k[HH_NL];
-    __shared__ uint16_t s_exc[HH_NL];
-    __shared__ uint32_t s_cnt4[4];
-    __shared__ int32_t s_part[4][HH_KM];
-    __shared__ uint64_t s_out[HH_KM];
-    extern __shared__ uint32_t s_l2[];
-
-    const uint64_t tile = blockIdx.x;
-    const uint32_t lane = threadIdx.x;
-    TileGeom g = tile_geom(tile, S, bits);
-    stage_tables(s_l1, s_l2, tab);
-    stage_words(s_w, gdata, g.b0 >> 5, g.nw, nwords_ok);
-    __syncthreads();
-
-    hh_ctx c;
-    c.w = s_w; c.sh = (uint32_t)(g.b0 & 31); c.l1 = s_l1; c.l2 = s_l2;
-    c.tree = tab.tree; c.tsym = tab.tsym; c.bt = g.bt;
-
-    const uint32_t p0 = lane * S;
-    uint32_t n = 0, x = p0;
-    if (p0 < c.bt) x = hh_region_count(&c, p0, p0 + S, &n);
-    hh_rec r;
-    hh_walk(&c, lane, S, x, &r);
-    r.n = n;
-    rec[tile * HH_NL + lane] = hh_rec_pack(r);
-    if (r.k == 0) atomicOr(flags, (uint32_t)F_FAIL);
-    const uint32_t kk = r.k ? r.k : 1u;
-
-    // live-lane sets for every entering d: bit d of s_mem[j] <=> lane j live
-    s_mem[lane] = lane >= HH_KM - 1 ? 0xffu : (uint8_t)((1u << (lane + 1)) - 1u);
-    s_k[lane] = (uint8_t)kk;
-    uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt4);
-    if (lane == 0) {
-        for (uint32_t i = 0; i < nexc; i++) {
-            uint32_t j = s_exc[i];
-            uint32_t kj = s_k[j];
-            uint8_t m = s_mem[j];
-            for (uint32_t q = j + 1; q < j + kj && q < HH_NL; q++) s_mem[q] &= (uint8_t)~m;
-        }
-    }
-    __syncthreads();
-    const uint32_t mem = s_mem[lane];
-    const int32_t contrib = (int32_t)(r.n + r.cov) + (lane + kk < HH_NL ? r.delta : 0);
-    if (lane + kk >= HH_NL) {
-        for (uint32_t d = 0; d < HH_KM; d++)
-            if ((mem >> d) & 1u) s_out[d] = hh_xf_pack(0, r.delta, r.e, lane + kk - HH_NL);
-    }
-#pragma unroll
-    for (uint32_t d = 0; d < HH_KM; d++) {
-        int32_t v = ((mem >> d) & 1u) ? contrib : 0;
-        v = (int32_t)wave_sum((uint32_t)v);
-        if ((lane & 63) == 0) s_part[lane >> 6][d] = v;
-    }
-    __syncthreads();
-    if (lane < HH_KM) {
-        int32_t cnt = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane];
-        uint64_t o = s_out[lane];
-        ttab[tile * HH_KM + lane] = hh_xf_pack((uint32_t)cnt, hh_xf_delta(o), hh_xf_e(o), hh_xf_d(o));
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K2: ordered composition of tile tables -> entering state of every tile.
-// state[t] = {d | e<<8 | delta<<32, base}; state[ntiles] holds the total.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(HH_SCAN_T) void k_scan(const uint64_t *__restrict__ ttab, uint64_t ntiles,
-                                                    uint64_t *__restrict__ state, uint32_t *flags) {
-    __shared__ hh_fn s_agg[HH_SCAN_T];
-    __shared__ uint64_t s_pre[HH_SCAN_T][2];
-    const uint32_t t = threadIdx.x;
-    const uint64_t per = (ntiles + HH_SCAN_T - 1) / HH_SCAN_T;
-    const uint64_t t0 = t * per;
-    const uint64_t t1 = t0 + per < ntiles ? t0 + per : ntiles;
-    if (t0 < t1) {
-        hh_fn f;
-        hh_fn_from_tab(&ttab[t0 * HH_KM], &f);
-        for (uint64_t i = t0 + 1; i < t1; i++) {
-            hh_fn gfn;
-            hh_fn_from_tab(&ttab[i * HH_KM], &gfn);
-            hh_fn_compose(&f, &gfn, &f);
-        }
-        s_agg[t] = f;
-    }
-    __syncthreads();
-    if (t == 0) {
-        hh_state s = {0, 0, 0, 0};
-        for (uint32_t i = 0; i < HH_SCAN_T; i++) {
-            s_pre[i][0] = (uint64_t)s.d | ((uint64_t)s.e << 8) | ((uint64_t)(uint32_t)s.delta << 32);
-            s_pre[i][1] = s.base;
-            if (i * per < ntiles) s = hh_fn_apply(&s_agg[i], s);
-        }
-        state[ntiles * 2] = (uint64_t)s.d | ((uint64_t)s.e << 8) | ((uint64_t)(uint32_t)s.delta << 32);
-        state[ntiles * 2 + 1] = s.base;
-        flags[2] = (uint32_t)s.base;
-        flags[3] = (uint32_t)(s.base >> 32);
-    }
-    __syncthreads();
-    if (t0 < t1) {
-        hh_state s;
-        uint64_t p = s_pre[t][0];
-        s.d = (uint32_t)(p & 0xff);
-        s.e = (uint32_t)((p >> 8) & 0xffffff);
-        s.delta = (int32_t)(uint32_t)(p >> 32);
-        s.base = s_pre[t][1];
-        for (uint64_t i = t0; i < t1; i++) {
-            state[i * 2] = (uint64_t)s.d | ((uint64_t)s.e << 8) | ((uint64_t)(uint32_t)s.delta << 32);
-            state[i * 2 + 1] = s.base;
-            s = hh_xf_apply(&ttab[i * HH_KM], s);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K3: emission of every live run through an LDS staging window.
-// ---------------------------------------------------------------------------
-struct StageSink {
-    uint8_t *stage;
-    uint64_t origin;   // output index of stage[0]
-    __device__ __forceinline__ void operator()(uint64_t o, uint32_t b) {
-        stage[o - origin] = (uint8_t)b;
-    }
+struct LookBack {
+    uint64_t *gran;      // [ntiles] tagged: table published + outgoing state if constant
+    uint64_t *cnt;       // [ntiles] tagged: 1 = aggregate count, 2 = inclusive prefix
+    uint64_t *tabs;      // [ntiles][HH_KM] tile tables (sc1 stores)
+    uint32_t *counter;   // tile dispenser
 };
 
-__global__ __launch_bounds__(HH_NL) void k_emit(const uint32_t *__restrict__ gdata, uint64_t bits,
-                                                uint64_t nwords_ok, uint32_t S, DevTab tab,
-                                                const uint64_t *__restrict__ rec,
-                                                const uint64_t *__restrict__ state,
-                                                uint8_t *__restrict__ out, uint64_t cap,
-                                                uint32_t *flags) {
+// 64-bit granules: the data is the flag (bits 62..63 = status, 0 = not yet).
+#define HH_ST_SHIFT 62
+#define HH_VAL_MASK ((1ull << HH_ST_SHIFT) - 1ull)
+#define HH_GR_CONST (1ull << 32)
+
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+enum { F_TIMEOUT = 8 };
+
+// Diagnostic build only (-DHH_STAMPS): wave 0 of every workgroup adds the
+// shader-clock cycles of each phase into dbg[block][phase].
+#ifdef HH_STAMPS
+#define HH_NSTAMP 8
+#define STAMP_DECL uint64_t st_acc[HH_NSTAMP] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(i) do { uint64_t t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_t; st_t = t_; } while (0)
+#define STAMP_FLUSH(dbg) do { if (threadIdx.x == 0) for (int i_ = 0; i_ < HH_NSTAMP; i_++) (dbg)[blockIdx.x * HH_NSTAMP + i_] = st_acc[i_]; } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH(dbg) do {} while (0)
+#endif
+#define HH_SPIN_LIMIT (1u << 22)
+
+__device__ __forceinline__ uint64_t state_pack(const hh_state &s) {
+    return (uint64_t)s.d | ((uint64_t)s.e << 8) | ((uint64_t)(uint32_t)s.delta << 32);
+}
+__device__ __forceinline__ hh_state state_unpack(uint64_t p, uint64_t base) {
+    hh_state s;
+    s.d = (uint32_t)(p & 0xff);
+    s.e = (uint32_t)((p >> 8) & 0xffffff);
+    s.delta = (int32_t)(uint32_t)(p >> 32);
+    s.base = base;
+    return s;
+}
+
+// Stage n u64 / u32 table words with all loads issued before any LDS store.
+template <uint32_t N>
+__device__ __forceinline__ void stage_l1(uint64_t *dst, const uint64_t *src) {
+    constexpr uint32_t PER = N / HH_NL;
+    uint64_t v[PER];
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) v[k] = src[threadIdx.x + k * HH_NL];
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) dst[threadIdx.x + k * HH_NL] = v[k];
+}
+
+__device__ __forceinline__ void stage_tile_words(uint32_t *s_w, const uint32_t *g, uint64_t w0,
+                                                 uint32_t nw, uint64_t nwords_ok) {
+    constexpr uint32_t PER = (HH_NW_MAX + HH_NL - 1) / HH_NL;
+    uint32_t v[PER];
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        uint32_t i = threadIdx.x + k * HH_NL;
+        uint64_t gi = w0 + i;
+        v[k] = (i < nw && gi < nwords_ok) ? __builtin_nontemporal_load(&g[gi]) : 0u;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < PER; k++) {
+        uint32_t i = threadIdx.x + k * HH_NL;
+        if (i < nw) s_w[i] = v[k];
+    }
+}
+
+// Decode the run [p, pe) for output indices [o, we) into stage[idx - org]:
+// whole dwords by ds_write_b32, the partial first / last dword by bytes (the
+// neighbouring run owns its other bytes).
+__device__ __forceinline__ void emit_run_lds(const hh_ctx *c, uint32_t &p, uint32_t pe, uint64_t &o,
+                                             uint64_t we, uint8_t *stage, uint64_t org) {
+    uint32_t q = (uint32_t)(o - org);
+    while ((q & 3u) && p < pe && o < we) {
+        uint32_t s;
+        p += hh_dec1(c, p, &s);
+        stage[q++] = (uint8_t)s;
+        o++;
+    }
+    uint32_t *st32 = (uint32_t *)stage;
+    uint64_t acc = 0;
+    uint32_t nacc = 0;
+    while (p < pe && o < we) {
+        uint32_t win = hh_read32(c, p);
+        uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
+        uint32_t ns = HH_L1_NSYM(e), val, n, adv;
+        if (ns && p + HH_L1_NBITS(e) <= pe && o + ns <= we) {
+            val = HH_L1_SYMS(e);
+            n = ns;
+            adv = HH_L1_NBITS(e);
+        } else {
+            uint32_t s;
+            adv = hh_dec1(c, p, &s);
+            val = s;
+            n = 1;
+        }
+        acc |= (uint64_t)val << (8u * nacc);
+        nacc += n;
+        o += n;
+        p += adv;
+        if (nacc >= 4) {
+            st32[q >> 2] = (uint32_t)acc;
+            acc >>= 32;
+            nacc -= 4;
+            q += 4;
+        }
+    }
+    for (uint32_t i = 0; i < nacc; i++) stage[q + i] = (uint8_t)(acc >> (8 * i));
+}
+
+// Poll a tagged granule until its status bits are non-zero (bounded).
+__device__ __forceinline__ uint64_t poll_granule(const uint64_t *p, uint32_t *flags) {
+    uint64_t v;
+    uint32_t spins = 0;
+    while (((v = ld_sc1(p)) >> HH_ST_SHIFT) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > HH_SPIN_LIMIT) {
+            atomicOr(flags, (uint32_t)F_TIMEOUT);
+            return 3ull << HH_ST_SHIFT;
+        }
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+
+// Emit the run [p, pe) to global memory at dst: dword stores, bytes for the
+// partial first / last dword (the neighbouring runs own their other bytes).
+__device__ __forceinline__ void emit_run_global(const hh_ctx *c, uint32_t p, uint32_t pe, uint8_t *dst) {
+    uintptr_t a = (uintptr_t)dst;
+    while ((a & 3u) && p < pe) {
+        uint32_t s;
+        p += hh_dec1(c, p, &s);
+        *(uint8_t *)a = (uint8_t)s;
+        a++;
+    }
+    uint64_t acc = 0;
+    uint32_t nacc = 0;
+    while (p < pe) {
+        uint32_t win = hh_read32(c, p);
+        uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
+        uint32_t ns = HH_L1_NSYM(e), val, n, adv;
+        if (ns && p + HH_L1_NBITS(e) <= pe) {
+            val = HH_L1_SYMS(e);
+            n = ns;
+            adv = HH_L1_NBITS(e);
+        } else {
+            uint32_t s;
+            adv = hh_dec1(c, p, &s);
+            val = s;
+            n = 1;
+        }
+        acc |= (uint64_t)val << (8u * nacc);
+        nacc += n;
+        p += adv;
+        if (nacc >= 4) {
+            *(uint32_t *)a = (uint32_t)acc;
+            a += 4;
+            acc >>= 32;
+            nacc -= 4;
+        }
+    }
+    for (uint32_t i = 0; i < nacc; i++) *(uint8_t *)(a + i) = (uint8_t)(acc >> (8 * i));
+}
+
+// Regions per tile: the last lane decodes the NEXT tile's first region too
+// (its mask lets the tile's last walk merge without a two-pointer walk).
+#define HH_NR (HH_NL - 1)
+
+__global__ __launch_bounds__(HH_NL) void k_decode(const uint32_t *__restrict__ gdata, uint64_t bits,
+                                                  uint64_t nwords_ok, uint32_t S, DevTab tab,
+                                                  uint64_t ntiles, LookBack lb,
+                                                  uint8_t *__restrict__ out, uint64_t cap,
+                                                  uint32_t *flags, uint32_t diag_stop,
+                                                  uint64_t *dbg) {
     __shared__ uint64_t s_l1[HH_L1_SIZE];
     __shared__ uint32_t s_w[HH_NW_MAX];
-    __shared__ __attribute__((aligned(16))) uint8_t s_stage[HH_CAP];
+    __shared__ uint32_t s_mask[HH_NL * HH_MW_MAX];
+    __shared__ uint16_t s_x[HH_NL];
+    __shared__ uint16_t s_n[HH_NL];
     __shared__ uint8_t s_mem[HH_NL];
     __shared__ uint8_t s_k[HH_NL];
     __shared__ uint16_t s_exc[HH_NL];
     __shared__ uint16_t s_ein[HH_NL];
     __shared__ int16_t s_din[HH_NL];
     __shared__ uint32_t s_cnt4[4];
+    __shared__ int32_t s_part[4][HH_KM];
+    __shared__ uint64_t s_out[HH_KM];
+    __shared__ uint64_t s_tab[HH_KM];
+    __shared__ uint64_t s_state[2];
+    __shared__ uint32_t s_tile;
     extern __shared__ uint32_t s_l2[];
 
-    const uint64_t tile = blockIdx.x;
     const uint32_t lane = threadIdx.x;
-    TileGeom g = tile_geom(tile, S, bits);
-    stage_tables(s_l1, s_l2, tab);
-    stage_words(s_w, gdata, g.b0 >> 5, g.nw, nwords_ok);
-    const hh_rec r = hh_rec_unpack(rec[tile * HH_NL + lane]);
-    const uint32_t kk = r.k ? r.k : 1u;
-    const uint64_t sp = state[tile * 2];
-    const uint32_t d_in = (uint32_t)(sp & 0xff);
-    const uint32_t e_tile = (uint32_t)((sp >> 8) & 0xffffff);
-    const int32_t del_tile = (int32_t)(uint32_t)(sp >> 32);
-    const uint64_t base = state[tile * 2 + 1];
-    const uint64_t base_next = state[tile * 2 + 3];
+    const uint32_t mw = (S + 31) / 32;
+    stage_l1<HH_L1_SIZE>(s_l1, tab.l1);
+    for (uint32_t i = lane; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
+    STAMP_DECL
 
-    s_mem[lane] = lane >= d_in;
-    s_k[lane] = (uint8_t)kk;
-    uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt4);   // syncs
-    if (lane == 0) {
-        for (uint32_t i = 0; i < nexc; i++) {
-            uint32_t j = s_exc[i];
-            if (!s_mem[j]) continue;
-            uint32_t kj = s_k[j];
-            for (uint32_t q = j + 1; q < j + kj && q < HH_NL; q++) s_mem[q] = 0;
+    for (;;) {
+        if (lane == 0) s_tile = atomicAdd(lb.counter, 1u);
+        __syncthreads();                       // also fences LDS reuse
+        const uint64_t tile = s_tile;
+        if (tile >= ntiles) break;
+        STAMP(0);
+        TileGeom g;
+        g.b0 = tile * (uint64_t)HH_NR * S;
+        {
+            const uint32_t span = (HH_NL + HH_KM + 1) * S + HH_SPAN_MARGIN;
+            g.nw = (span + 31) / 32 + 3;
+            const uint64_t rem = bits - g.b0;
+            g.bt = rem < span ? (uint32_t)rem : span;
         }
-    }
-    __syncthreads();
-    const bool live = s_mem[lane] != 0;
-    if (live && lane + kk < HH_NL) {
-        s_ein[lane + kk] = (uint16_t)r.e;
-        s_din[lane + kk] = (int16_t)r.delta;
-    }
-    __syncthreads();
-    uint32_t e_in = 0;
-    int32_t del_in = 0;
-    if (live) {
-        e_in = lane == d_in ? e_tile : s_ein[lane];
-        del_in = lane == d_in ? del_tile : s_din[lane];
-    }
-    const uint32_t cnt = live ? (uint32_t)((int32_t)(r.n + r.cov) + del_in) : 0u;
-    uint32_t total;
-    const uint32_t off = block_excl_scan(cnt, s_cnt4, &total);
-    if (lane == 0 && base + total != base_next) atomicOr(flags, (uint32_t)F_MISMATCH);
-
-    hh_ctx c;
-    c.w = s_w; c.sh = (uint32_t)(g.b0 & 31); c.l1 = s_l1; c.l2 = s_l2;
-    c.tree = tab.tree; c.tsym = tab.tsym; c.bt = g.bt;
-    uint32_t p = lane * S + e_in;
-    const uint32_t end = (lane + kk) * S + r.e;
-    const uint32_t pe = live ? (end < c.bt ? end : c.bt) : 0u;
-    uint64_t o = base + off;
-
-    // window in absolute addresses; never write at or beyond out + cap
-    const uint64_t oaddr = (uint64_t)(uintptr_t)out;
-    uint64_t hi_idx = base + total;
-    if (hi_idx > cap) {
-        if (lane == 0) atomicOr(flags, (uint32_t)F_OVER);
-        hi_idx = cap;
-    }
-    if (base >= hi_idx) return;
-    const uint64_t lo = oaddr + base, hi = oaddr + hi_idx;
-    const uint64_t a0 = lo & ~(uint64_t)15;
-    const uint32_t nrounds = (uint32_t)((hi - a0 + HH_CAP - 1) / HH_CAP);
-    for (uint32_t rd = 0; rd < nrounds; rd++) {
-        const uint64_t wa = a0 + (uint64_t)rd * HH_CAP;
-        const uint64_t wend_idx = (wa + HH_CAP < hi ? wa + HH_CAP : hi) - oaddr;
-        StageSink sink{s_stage, wa - oaddr};
-        if (p < pe && o < wend_idx) hh_emit_run(&c, &p, pe, &o, wend_idx, sink);
+        stage_tile_words(s_w, gdata, g.b0 >> 5, g.nw, nwords_ok);
         __syncthreads();
-        for (uint32_t ch = lane; ch < HH_CAP / 16; ch += HH_NL) {
-            uint64_t a = wa + 16ull * ch;
-            if (a >= hi || a + 16 <= lo) continue;
-            if (a >= lo && a + 16 <= hi) {
-                *(uint4 *)(uintptr_t)a = *(const uint4 *)&s_stage[16 * ch];
+        STAMP(1);
+
+        hh_ctx c;
+        c.w = s_w; c.sh = (uint32_t)(g.b0 & 31); c.l1 = s_l1; c.l2 = s_l2;
+        c.tree = tab.tree; c.tsym = tab.tsym; c.bt = g.bt;
+
+        // (2) region decode from offset 0 (+ boundary mask), all NL lanes
+        const uint32_t p0 = lane * S;
+        uint32_t n = 0, x = p0;
+        {
+            struct MS {
+                uint32_t *m;
+                __device__ void operator()(uint32_t w, uint32_t v) { m[w] = v; }
+            } ms{&s_mask[lane * mw]};
+            if (p0 < c.bt) {
+                x = hh_region_count_mask(&c, p0, p0 + S, mw, &n, ms);
             } else {
-                for (uint32_t b = 0; b < 16; b++)
-                    if (a + b >= lo && a + b < hi) *(uint8_t *)(uintptr_t)(a + b) = s_stage[16 * ch + b];
+                for (uint32_t w2 = 0; w2 < mw; w2++) s_mask[lane * mw + w2] = 0;
+            }
+        }
+        s_x[lane] = (uint16_t)(x - p0);
+        s_n[lane] = (uint16_t)n;
+        __syncthreads();
+        STAMP(2);
+        hh_rec r;
+        r.n = n; r.k = 1; r.e = 0; r.delta = 0; r.cov = 0;
+        if (lane < HH_NR) {
+            hh_masks mk = {s_mask, s_x, s_n, HH_NL, mw};
+            hh_walk_mask(&c, &mk, lane, S, x, &r);
+            r.n = n;
+            if (r.k == 0) atomicOr(flags, (uint32_t)F_FAIL);
+        }
+        const uint32_t kk = r.k ? r.k : 1u;
+        STAMP(3);
+
+        // (3) live regions for every entering d -> transfer table
+        s_mem[lane] = lane >= HH_NR ? 0u : (lane >= HH_KM - 1 ? 0xffu : (uint8_t)((1u << (lane + 1)) - 1u));
+        s_k[lane] = (uint8_t)kk;
+        const uint32_t nexc = collect_exceptions(kk > 1 && lane < HH_NR, s_exc, s_cnt4);
+        if (lane == 0) {
+            for (uint32_t i = 0; i < nexc; i++) {
+                uint32_t j = s_exc[i], kj = s_k[j];
+                uint8_t m = s_mem[j];
+                for (uint32_t q = j + 1; q < j + kj && q < HH_NR; q++) s_mem[q] &= (uint8_t)~m;
             }
         }
         __syncthreads();
+        const uint32_t memd = s_mem[lane];
+        const int32_t contrib = (int32_t)(r.n + r.cov) + (lane + kk < HH_NR ? r.delta : 0);
+        if (lane < HH_NR && lane + kk >= HH_NR) {
+            for (uint32_t d = 0; d < HH_KM; d++)
+                if ((memd >> d) & 1u) s_out[d] = hh_xf_pack(0, r.delta, r.e, lane + kk - HH_NR);
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < HH_KM; d++) {
+            int32_t v = ((memd >> d) & 1u) ? contrib : 0;
+            v = (int32_t)wave_sum((uint32_t)v);
+            if ((lane & 63) == 0) s_part[lane >> 6][d] = v;
+        }
+        __syncthreads();
+        if (lane < HH_KM) {
+            int32_t cnt = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane];
+            uint64_t o = s_out[lane];
+            s_tab[lane] = hh_xf_pack((uint32_t)cnt, hh_xf_delta(o), hh_xf_e(o), hh_xf_d(o));
+        }
+        __syncthreads();
+        STAMP(4);
+        // (4a) publish the table (sc1) and its granule: outgoing state if
+        // every entering d leads to the same one (the normal case).
+        if (lane == 0) {
+            uint64_t o0 = s_tab[0] >> 32;
+            bool cst = true;
+            for (uint32_t i = 0; i < HH_KM; i++) {
+                st_sc1(&lb.tabs[tile * HH_KM + i], s_tab[i]);
+                cst = cst && (s_tab[i] >> 32) == o0;
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint64_t o = s_tab[0];
+            uint64_t gr = (uint64_t)hh_xf_d(o) | ((uint64_t)hh_xf_e(o) << 4) |
+                          ((uint64_t)((uint32_t)hh_xf_delta(o) & 0xffffu) << 16) |
+                          (cst ? HH_GR_CONST : 0ull) | (1ull << HH_ST_SHIFT);
+            st_sc1(&lb.gran[tile], gr);
+            // (4b) entering state from the predecessor's granule
+            hh_state sin = {0, 0, 0, 0};
+            if (tile > 0) {
+                int64_t j = (int64_t)tile - 1;
+                uint64_t gj = poll_granule(&lb.gran[j], flags);
+                while (!(gj & HH_GR_CONST) && j > 0) {      // rare: walk back
+                    j--;
+                    gj = poll_granule(&lb.gran[j], flags);
+                }
+                int64_t m;
+                if (gj & HH_GR_CONST) {
+                    sin.d = (uint32_t)(gj & 0xf);
+                    sin.e = (uint32_t)((gj >> 4) & 0xfff);
+                    sin.delta = (int32_t)(int16_t)(uint16_t)(gj >> 16);
+                    m = j + 1;
+                } else {
+                    m = 0;                                   // from tile 0's entry
+                }
+                for (; m < (int64_t)tile; m++) {             // apply tables forward
+                    uint64_t v = ld_sc1(&lb.tabs[m * HH_KM + sin.d]);
+                    sin.d = hh_xf_d(v);
+                    sin.e = hh_xf_e(v);
+                    sin.delta = hh_xf_delta(v);
+                }
+            }
+            const uint64_t mycnt = (uint64_t)((int64_t)hh_xf_count(s_tab[sin.d]) + sin.delta);
+            s_state[0] = state_pack(sin);
+            s_state[1] = mycnt;
+        }
+        __syncthreads();
+        // (4c) output base: decoupled look-back over tagged counts, one wave
+        if (lane < 64) {
+            const uint64_t mycnt = s_state[1];
+            uint64_t excl = 0;
+            if (tile == 0) {
+                if (lane == 0) st_sc1(&lb.cnt[0], mycnt | (2ull << HH_ST_SHIFT));
+            } else {
+                if (lane == 0) st_sc1(&lb.cnt[tile], mycnt | (1ull << HH_ST_SHIFT));
+                int64_t top = (int64_t)tile - 1;
+                for (;;) {
+                    const int64_t idx = top - (int64_t)lane;
+                    uint64_t w = idx >= 0 ? ld_sc1(&lb.cnt[idx]) : (2ull << HH_ST_SHIFT);
+                    uint32_t spins = 0;
+                    uint32_t first;
+                    for (;;) {
+                        const uint32_t stv = (uint32_t)(w >> HH_ST_SHIFT);
+                        const uint64_t incl = __ballot(stv >= 2);
+                        const uint64_t zero = __ballot(stv == 0);
+                        first = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
+                        const uint64_t rel = first < 63 ? ((2ull << first) - 1ull) : ~0ull;
+                        if (!(zero & rel)) break;
+                        if (stv == 0 && idx >= 0) w = ld_sc1(&lb.cnt[idx]);
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins > HH_SPIN_LIMIT) {
+                            if (lane == 0) atomicOr(flags, (uint32_t)F_TIMEOUT);
+                            first = 0;
+                            w = 2ull << HH_ST_SHIFT;
+                            break;
+                        }
+                    }
+                    const uint64_t v = lane <= first ? (w & HH_VAL_MASK) : 0ull;
+                    excl += wave_sum64(v);
+                    if (first < 64) break;
+                    top -= 64;
+                }
+                if (lane == 0) st_sc1(&lb.cnt[tile], (excl + mycnt) | (2ull << HH_ST_SHIFT));
+            }
+            if (lane == 0) {
+                if (tile == ntiles - 1) {
+                    flags[2] = (uint32_t)(excl + mycnt);
+                    flags[3] = (uint32_t)((excl + mycnt) >> 32);
+                }
+                s_state[1] = excl;
+            }
+        }
+        __syncthreads();
+        const hh_state sin = state_unpack(s_state[0], s_state[1]);
+        STAMP(5);
+
+        // (5) live regions of this tile and their runs, emitted to global
+        s_mem[lane] = lane >= sin.d && lane < HH_NR;
+        __syncthreads();
+        if (lane == 0) {
+            for (uint32_t i = 0; i < nexc; i++) {
+                uint32_t j = s_exc[i], kj = s_k[j];
+                if (!s_mem[j]) continue;
+                for (uint32_t q = j + 1; q < j + kj && q < HH_NR; q++) s_mem[q] = 0;
+            }
+        }
+        __syncthreads();
+        const bool live = s_mem[lane] != 0;
+        if (live && lane + kk < HH_NR) {
+            s_ein[lane + kk] = (uint16_t)r.e;
+            s_din[lane + kk] = (int16_t)r.delta;
+        }
+        __syncthreads();
+        uint32_t e_in = 0;
+        int32_t del_in = 0;
+        if (live) {
+            e_in = lane == sin.d ? sin.e : s_ein[lane];
+            del_in = lane == sin.d ? sin.delta : s_din[lane];
+        }
+        const uint32_t cnt = live ? (uint32_t)((int32_t)(r.n + r.cov) + del_in) : 0u;
+        uint32_t total;
+        const uint32_t off = block_excl_scan(cnt, s_cnt4, &total);
+        const uint64_t base = sin.base;
+        if (base + total > cap) {
+            if (lane == 0) atomicOr(flags, (uint32_t)F_OVER);
+        } else if (live) {
+            const uint32_t start = lane * S + e_in;
+            const uint32_t end = (lane + kk) * S + r.e;
+            const uint32_t pe = end < c.bt ? end : c.bt;
+            if (start < pe) emit_run_global(&c, start, pe, out + base + off);
+        }
+        STAMP(6);
     }
+    STAMP_FLUSH(dbg);
 }
 
 // ---------------------------------------------------------------------------
@@ -472,6 +683,10 @@ struct hh_decoder {
     uint32_t *h_flags;   // pinned
     hipEvent_t ev[4];
     hh_stats stats;
+    uint32_t grid;       // persistent grid size (occupancy x CUs)
+    size_t grid_l2b;     // dynamic LDS the grid was sized for
+    uint32_t diag_stop;  // HIPHUFF_DIAG_STOP: time the phases (diagnostic only)
+    uint64_t *d_dbg;     // per-block phase cycles (HH_STAMPS builds)
 };
 
 static int ensure_ws(hh_decoder *d, size_t need) {
@@ -510,6 +725,8 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
         return HH_ERR_DEVICE;
     }
     for (int i = 0; i < 4; i++) hipEventCreate(&d->ev[i]);
+    const char *ds = getenv("HIPHUFF_DIAG_STOP");
+    d->diag_stop = ds ? (uint32_t)atoi(ds) : 0u;
     *out = d;
     return HH_OK;
 }
@@ -518,6 +735,7 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
     if (!d) return;
     hipSetDevice(d->device);
     if (d->ws) hipFree(d->ws);
+    if (d->d_dbg) hipFree(d->d_dbg);
     if (d->d_l1) hipFree(d->d_l1);
     if (d->d_l2) hipFree(d->d_l2);
     if (d->d_tree) hipFree(d->d_tree);
@@ -596,51 +814,61 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
         return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
     }
     const uint32_t S = d->S;
-    const uint64_t tb = (uint64_t)HH_NL * S;
+    const uint64_t tb = (uint64_t)HH_NR * S;
     const uint64_t ntiles = (bits + tb - 1) / tb;
     const uint64_t nwords_ok = ((bits + 7) / 8 + HH_PAYLOAD_PAD) / 4;
-    size_t need = 64 + ntiles * HH_NL * 8 + ntiles * HH_KM * 8 + (ntiles + 1) * 16 + 256;
+    // workspace: [flags 64 B | counter, granules, counts (zeroed) | tables]
+    const size_t zero_bytes = (16 + ntiles * 16 + 15) & ~(size_t)15;
+    size_t need = 64 + zero_bytes + ntiles * HH_KM * 8 + 256;
     int rc = ensure_ws(d, need);
     if (rc) return rc;
     uint8_t *w = (uint8_t *)d->ws;
     uint32_t *d_flags = (uint32_t *)w;
-    uint64_t *d_rec = (uint64_t *)(w + 64);
-    uint64_t *d_tab = d_rec + ntiles * HH_NL;
-    uint64_t *d_state = d_tab + ntiles * HH_KM;
+    LookBack lb;
+    lb.counter = (uint32_t *)(w + 64);
+    lb.gran = (uint64_t *)(w + 64 + 16);
+    lb.cnt = lb.gran + ntiles;
+    lb.tabs = (uint64_t *)(w + 64 + zero_bytes);
     const size_t l2b = sizeof(uint32_t) * d->tab.l2_used;
+    if (!d->grid || d->grid_l2b != l2b) {
+        int per_cu = 0, ncu = 0;
+        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode, HH_NL, l2b));
+        d->grid_l2b = l2b;
+        if (d->d_dbg) HIP_OK(hipFree(d->d_dbg));
+        HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
+        d->grid = (uint32_t)((per_cu > 0 ? per_cu : 1) * ncu);
+        HIP_OK(hipMalloc(&d->d_dbg, (size_t)d->grid * 8 * sizeof(uint64_t)));
+        HIP_OK(hipMemset(d->d_dbg, 0, (size_t)d->grid * 8 * sizeof(uint64_t)));
+    }
+    const uint32_t grid = (uint32_t)(ntiles < d->grid ? ntiles : d->grid);
 
-    HIP_OK(hipMemsetAsync(d_flags, 0, 64, st));
+    HIP_OK(hipMemsetAsync(d_flags, 0, 64 + zero_bytes, st));
     HIP_OK(hipEventRecord(d->ev[0], st));
-    hipLaunchKernelGGL(k_sync, dim3((unsigned)ntiles), dim3(HH_NL), l2b, st, (const uint32_t *)d_data,
-                       bits, nwords_ok, S, d->tab, d_rec, d_tab, d_flags);
+    hipLaunchKernelGGL(k_decode, dim3(grid), dim3(HH_NL), l2b, st, (const uint32_t *)d_data, bits,
+                       nwords_ok, S, d->tab, ntiles, lb, (uint8_t *)d_out, cap, d_flags, d->diag_stop,
+                       d->d_dbg);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d->ev[1], st));
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(HH_SCAN_T), 0, st, d_tab, ntiles, d_state, d_flags);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(d->ev[2], st));
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)ntiles), dim3(HH_NL), l2b, st, (const uint32_t *)d_data,
-                       bits, nwords_ok, S, d->tab, d_rec, d_state, (uint8_t *)d_out, cap, d_flags);
-    HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(d->ev[3], st));
     HIP_OK(hipMemcpyAsync(d->h_flags, d_flags, 16, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     const uint32_t fl = d->h_flags[0];
     const uint64_t total = (uint64_t)d->h_flags[2] | ((uint64_t)d->h_flags[3] << 32);
-    float ms[3];
-    for (int i = 0; i < 3; i++) hipEventElapsedTime(&ms[i], d->ev[i], d->ev[i + 1]);
-    d->stats.ms_sync = ms[0];
-    d->stats.ms_scan = ms[1];
-    d->stats.ms_emit = ms[2];
-    d->stats.ms_total = ms[0] + ms[1] + ms[2];
-    d->stats.lanes = ntiles * HH_NL;
+    float ms = 0;
+    hipEventElapsedTime(&ms, d->ev[0], d->ev[1]);
+    d->stats.ms_total = ms;
+    d->stats.ms_sync = 0;
+    d->stats.ms_scan = 0;
+    d->stats.ms_emit = ms;
+    d->stats.lanes = ntiles * HH_NR;
     d->stats.out_len = total;
+    if (d->diag_stop) { *out_len = 0; return HH_OK; }
+    if (fl & F_TIMEOUT) return HH_ERR_TIMEOUT;
     if (fl & F_FAIL) {
         // A walk found no shared boundary within HH_KM regions: the code does
         // not resynchronise (non-synchronising code) -- take the exact path.
         d->stats.exact_fallback = 1;
         return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
     }
-    if (fl & F_MISMATCH) return HH_ERR_INTERNAL;
     *out_len = total;
     if (total > cap) return HH_ERR_CAPACITY;
     return HH_OK;
@@ -804,4 +1032,14 @@ extern "C" int hh_stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits
     HIP_OK(hipSetDevice(d->device));
     hipStream_t st = s ? (hipStream_t)s : d->stream;
     return stage_pipeline(d, d_data, bits, d_out, cap, out_len, st);
+}
+
+// Diagnostic: per-block phase cycle sums of the last decode (HH_STAMPS
+// builds; zeros otherwise).  Returns the number of blocks written.
+extern "C" int hh_debug_phase_cycles(hh_decoder *d, uint64_t *out, int max_blocks) {
+    if (!d || !out || !d->d_dbg) return 0;
+    int n = (int)d->grid < max_blocks ? (int)d->grid : max_blocks;
+    if (hipMemcpy(out, d->d_dbg, (size_t)n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return HH_ERR_DEVICE;
+    return n;
 }

@@ -156,8 +156,9 @@ int hh_tree_check(const hh_tree *t, hh_tree_info *info) {
     if (!t || t->nodes <= 0 || !t->izero || !t->ione || !t->sym) return HH_ERR_ARG;
     const int32_t n = t->nodes;
     uint8_t *seen = (uint8_t *)calloc((size_t)n, 1);
-    int32_t *stk = (int32_t *)malloc(sizeof(int32_t) * 2 * ((size_t)n + 1));
-    int32_t *dep = stk + n + 1;
+    /* every pop of an unseen node pushes two: at most 2n + 1 entries */
+    int32_t *stk = (int32_t *)malloc(sizeof(int32_t) * 2 * (2 * (size_t)n + 2));
+    int32_t *dep = stk + 2 * (size_t)n + 2;
     if (!seen || !stk) { free(seen); free(stk); return HH_ERR_NOMEM; }
     hh_tree_info in = {0, 0, 1 << 30, 0, 0};
     int sp = 0, rc = HH_OK;
@@ -339,13 +340,14 @@ int hh_tables_build(const void *tree_v, hh_tables *T) {
 
     /* L1: walk HH_P bits of the index, collect up to HH_K complete symbols */
     for (uint32_t w = 0; w < HH_L1_SIZE; w++) {
-        uint32_t node = 0, syms = 0, nsym = 0, nbits = 0, len0 = 0;
+        uint32_t node = 0, syms = 0, nsym = 0, nbits = 0, len0 = 0, bmask = 0;
         unsigned pos = 0, start = 0;
         while (pos < HH_P && nsym < HH_K) {
             node = tchild(T, node, (w >> pos) & 1);
             pos++;
             if (tleaf(T, node)) {
                 syms |= (uint32_t)T->tsym[node] << (8 * nsym);
+                bmask |= 1u << start;
                 if (nsym == 0) len0 = pos - start;
                 nsym++;
                 nbits = pos;
@@ -356,7 +358,7 @@ int hh_tables_build(const void *tree_v, hh_tables *T) {
         uint64_t e;
         if (nsym) {
             e = (uint64_t)syms | ((uint64_t)nbits << 32) | ((uint64_t)nsym << 37) |
-                ((uint64_t)len0 << 40);
+                ((uint64_t)len0 << 40) | ((uint64_t)bmask << 45);
         } else {
             /* node is the internal node at depth HH_P on the path of w */
             int q = subtree_height(T, node, HH_Q_MAX);

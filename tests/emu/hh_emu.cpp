@@ -6,6 +6,7 @@
 // product links this file; it builds into tests/emu/libhh_emu.so.
 #include <stdint.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <vector>
@@ -55,16 +56,41 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
         c.bt = rem < span ? (uint32_t)rem : span;
     };
 
-    // K1: per lane count + walk, per tile table
+    // K1: per lane count + walk, per tile table.  The mask walk (what the
+    // kernel runs) is checked against the two-pointer walk on every lane.
+    const uint32_t mw = (S + 31) / 32;
+    std::vector<uint32_t> mask(HH_NL * mw);
+    std::vector<uint16_t> mx(HH_NL), mn(HH_NL);
+    std::vector<uint32_t> xs(HH_NL), ns(HH_NL);
     for (uint64_t t = 0; t < ntiles; t++) {
         hh_ctx c;
         load_tile(t, c);
         for (uint32_t lane = 0; lane < HH_NL; lane++) {
             uint32_t p0 = lane * S;
-            hh_rec r;
-            uint32_t n = 0, x = p0;
-            if (p0 < c.bt) x = hh_region_count(&c, p0, p0 + S, &n);
-            hh_walk(&c, lane, S, x, &r);
+            uint32_t n = 0, x = p0, n2 = 0, x2 = p0;
+            struct MS { uint32_t *m; void operator()(uint32_t w, uint32_t v) { m[w] = v; } } ms{&mask[lane * mw]};
+            for (uint32_t w2 = 0; w2 < mw; w2++) mask[lane * mw + w2] = 0;
+            if (p0 < c.bt) {
+                x = hh_region_count(&c, p0, p0 + S, &n);
+                x2 = hh_region_count_mask(&c, p0, p0 + S, mw, &n2, ms);
+                if (x2 != x || n2 != n) return HH_ERR_INTERNAL;
+            }
+            xs[lane] = x; ns[lane] = n;
+            mx[lane] = (uint16_t)(x - p0 - (x >= p0 + S ? S : 0));
+            mx[lane] = (uint16_t)(x >= p0 + S ? x - (p0 + S) + S : x - p0);
+            mn[lane] = (uint16_t)n;
+        }
+        hh_masks mk = {mask.data(), mx.data(), mn.data(), HH_NL, mw};
+        for (uint32_t lane = 0; lane < HH_NL; lane++) {
+            hh_rec r, r2;
+            hh_walk(&c, lane, S, xs[lane], &r);
+            hh_walk_mask(&c, &mk, lane, S, xs[lane], &r2);
+            if (r.k != r2.k || r.e != r2.e || r.delta != r2.delta || r.cov != r2.cov) {
+                fprintf(stderr, "walk mismatch tile %lu lane %u x=%u S=%u bt=%u: 2ptr k=%u e=%u d=%d cov=%u | mask k=%u e=%u d=%d cov=%u\n",
+                        (unsigned long)t, lane, xs[lane], S, c.bt, r.k, r.e, r.delta, r.cov, r2.k, r2.e, r2.delta, r2.cov);
+                return HH_ERR_INTERNAL - 100;
+            }
+            uint32_t n = ns[lane];
             r.n = n;
             if (r.k == 0) stats[2]++;
             if (r.k > 1) stats[1]++;
