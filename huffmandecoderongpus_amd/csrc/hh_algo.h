@@ -478,15 +478,15 @@ HH_HD hh_state hh_fn_apply(const hh_fn *f, hh_state s) {
 /* ------------------------------------------------------------------ */
 HH_HD uint32_t hh_rec_next(uint32_t j, const hh_rec &r) { return j + (r.k ? r.k : 1u); }
 
-/* Tile table: for each entering d, follow the live lanes j -> j + k_j. */
-HH_HD void hh_tile_table_seq(const uint64_t *rec, uint64_t *tab) {
+/* Tile table over nr regions: for each entering d, follow j -> j + k_j. */
+HH_HD void hh_tile_table_seq(const uint64_t *rec, uint32_t nr, uint64_t *tab) {
     for (uint32_t d = 0; d < HH_KM; d++) {
         uint32_t j = d, cnt = 0;
         for (;;) {
             hh_rec r = hh_rec_unpack(rec[j]);
             uint32_t nx = hh_rec_next(j, r);
             cnt += r.n + r.cov;
-            if (nx >= HH_NL) { tab[d] = hh_xf_pack(cnt, r.delta, r.e, nx - HH_NL); break; }
+            if (nx >= nr) { tab[d] = hh_xf_pack(cnt, r.delta, r.e, nx - nr); break; }
             cnt = (uint32_t)((int32_t)cnt + r.delta);
             j = nx;
         }

@@ -487,6 +487,7 @@ __global__ __launch_bounds__(HH_NL) void k_decode(const uint32_t *__restrict__ g
             s_state[1] = mycnt;
         }
         __syncthreads();
+        STAMP(7);
         // (4c) output base: decoupled look-back over tagged counts, one wave
         if (lane < 64) {
             const uint64_t mycnt = s_state[1];

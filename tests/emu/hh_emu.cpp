@@ -1,12 +1,15 @@
-// hh_emu.cpp -- TEST-ONLY host emulation of the fast-path kernels.
+// hh_emu.cpp -- TEST-ONLY host emulation of the fused decode kernel.
 //
-// Runs the same per-lane building blocks as the HIP kernels (hh_algo.h) on
-// host arrays, tile by tile, lane by lane, so the stitching logic can be
-// checked against the oracle on machines without a GPU.  Nothing in the
+// Runs the kernel's per-lane building blocks (hh_algo.h) on host arrays with
+// the kernel's geometry -- tiles of HH_NL-1 regions, one auxiliary lane that
+// decodes the next tile's first region, boundary masks, mask walks, tile
+// transfer tables, ordered state application, emission -- so the stitching
+// logic is checked against the oracle without a GPU.  Every lane's mask walk
+// is also cross-checked against the plain two-pointer walk.  Nothing in the
 // product links this file; it builds into tests/emu/libhh_emu.so.
 #include <stdint.h>
-#include <stdlib.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -16,24 +19,29 @@
 
 extern "C" {
 
-// stats[0]=tiles stats[1]=walks with k>1 stats[2]=failed walks
-// stats[3]=max k seen
+// stats[0]=tiles stats[1]=walks with k>1 stats[2]=failed walks stats[3]=max k
 int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *sym,
                       int32_t nodes, const uint8_t *data, uint64_t bits, uint32_t S,
                       uint8_t *out, uint64_t cap, int64_t *stats) {
+    const uint32_t NR = HH_NL - 1;
     hh_tree tree = {nodes, izero, ione, sym};
     static hh_tables T;   // large; not reentrant (test helper)
     int rc = hh_tables_build(&tree, &T);
     if (rc) return rc;
     for (int i = 0; i < 4; i++) stats[i] = 0;
     if (bits == 0) return 0;
-    const uint64_t TB = (uint64_t)HH_NL * S;
+    if (S < 2 || S > 32 * HH_MW_MAX) return HH_ERR_ARG;
+    const uint64_t TB = (uint64_t)NR * S;
     const uint64_t ntiles = (bits + TB - 1) / TB;
     const uint64_t nbytes = (bits + 7) / 8;
     const uint32_t span = (HH_NL + HH_KM + 1) * S + 320;  // bits a tile may touch
     const uint32_t nw = span / 32 + 3;
+    const uint32_t mw = (S + 31) / 32;
     std::vector<uint32_t> w(nw);
-    std::vector<uint64_t> rec((size_t)ntiles * HH_NL), tab((size_t)ntiles * HH_KM);
+    std::vector<uint64_t> rec((size_t)ntiles * NR), tab((size_t)ntiles * HH_KM);
+    std::vector<uint32_t> mask(HH_NL * mw);
+    std::vector<uint16_t> mx(HH_NL), mn(HH_NL);
+    std::vector<uint32_t> xs(HH_NL), ns(HH_NL);
     stats[0] = (int64_t)ntiles;
 
     auto load_tile = [&](uint64_t t, hh_ctx &c) {
@@ -56,59 +64,54 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
         c.bt = rem < span ? (uint32_t)rem : span;
     };
 
-    // K1: per lane count + walk, per tile table.  The mask walk (what the
-    // kernel runs) is checked against the two-pointer walk on every lane.
-    const uint32_t mw = (S + 31) / 32;
-    std::vector<uint32_t> mask(HH_NL * mw);
-    std::vector<uint16_t> mx(HH_NL), mn(HH_NL);
-    std::vector<uint32_t> xs(HH_NL), ns(HH_NL);
     for (uint64_t t = 0; t < ntiles; t++) {
         hh_ctx c;
         load_tile(t, c);
-        for (uint32_t lane = 0; lane < HH_NL; lane++) {
+        for (uint32_t lane = 0; lane < HH_NL; lane++) {   // incl. the aux lane
             uint32_t p0 = lane * S;
-            uint32_t n = 0, x = p0, n2 = 0, x2 = p0;
-            struct MS { uint32_t *m; void operator()(uint32_t w, uint32_t v) { m[w] = v; } } ms{&mask[lane * mw]};
+            uint32_t n = 0, x = p0, n2 = 0;
+            struct MS {
+                uint32_t *m;
+                void operator()(uint32_t wi, uint32_t v) { m[wi] = v; }
+            } ms{&mask[lane * mw]};
             for (uint32_t w2 = 0; w2 < mw; w2++) mask[lane * mw + w2] = 0;
             if (p0 < c.bt) {
                 x = hh_region_count(&c, p0, p0 + S, &n);
-                x2 = hh_region_count_mask(&c, p0, p0 + S, mw, &n2, ms);
+                uint32_t x2 = hh_region_count_mask(&c, p0, p0 + S, mw, &n2, ms);
                 if (x2 != x || n2 != n) return HH_ERR_INTERNAL;
             }
-            xs[lane] = x; ns[lane] = n;
-            mx[lane] = (uint16_t)(x - p0 - (x >= p0 + S ? S : 0));
-            mx[lane] = (uint16_t)(x >= p0 + S ? x - (p0 + S) + S : x - p0);
+            xs[lane] = x;
+            ns[lane] = n;
+            mx[lane] = (uint16_t)(x - p0);
             mn[lane] = (uint16_t)n;
         }
         hh_masks mk = {mask.data(), mx.data(), mn.data(), HH_NL, mw};
-        for (uint32_t lane = 0; lane < HH_NL; lane++) {
+        for (uint32_t lane = 0; lane < NR; lane++) {
             hh_rec r, r2;
             hh_walk(&c, lane, S, xs[lane], &r);
             hh_walk_mask(&c, &mk, lane, S, xs[lane], &r2);
             if (r.k != r2.k || r.e != r2.e || r.delta != r2.delta || r.cov != r2.cov) {
-                fprintf(stderr, "walk mismatch tile %lu lane %u x=%u S=%u bt=%u: 2ptr k=%u e=%u d=%d cov=%u | mask k=%u e=%u d=%d cov=%u\n",
-                        (unsigned long)t, lane, xs[lane], S, c.bt, r.k, r.e, r.delta, r.cov, r2.k, r2.e, r2.delta, r2.cov);
+                fprintf(stderr, "walk mismatch tile %lu lane %u: 2ptr k=%u e=%u d=%d cov=%u | mask k=%u e=%u d=%d cov=%u\n",
+                        (unsigned long)t, lane, r.k, r.e, r.delta, r.cov, r2.k, r2.e, r2.delta, r2.cov);
                 return HH_ERR_INTERNAL - 100;
             }
-            uint32_t n = ns[lane];
-            r.n = n;
-            if (r.k == 0) stats[2]++;
-            if (r.k > 1) stats[1]++;
-            if ((int64_t)r.k > stats[3]) stats[3] = r.k;
-            rec[t * HH_NL + lane] = hh_rec_pack(r);
+            r2.n = ns[lane];
+            if (r2.k == 0) stats[2]++;
+            if (r2.k > 1) stats[1]++;
+            if ((int64_t)r2.k > stats[3]) stats[3] = r2.k;
+            rec[t * NR + lane] = hh_rec_pack(r2);
         }
-        hh_tile_table_seq(&rec[t * HH_NL], &tab[t * HH_KM]);
+        hh_tile_table_seq(&rec[t * NR], NR, &tab[t * HH_KM]);
     }
     if (stats[2]) return HH_ERR_UNSUPPORTED;
 
-    // K2: scan over tile tables
+    // ordered application of the tile tables (the kernel's look-back)
     std::vector<hh_state> st(ntiles + 1);
     st[0] = hh_state{0, 0, 0, 0};
     for (uint64_t t = 0; t < ntiles; t++) st[t + 1] = hh_xf_apply(&tab[t * HH_KM], st[t]);
     uint64_t total = st[ntiles].base;
     if (total > cap) return HH_ERR_CAPACITY;
 
-    // K3: emission
     struct Sink {
         uint8_t *out;
         void operator()(uint64_t o, uint32_t b) { out[o] = (uint8_t)b; }
@@ -120,8 +123,8 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
         uint32_t j = s.d, e_in = s.e;
         int32_t del_in = s.delta;
         uint64_t o = s.base;
-        while (j < HH_NL) {
-            hh_rec r = hh_rec_unpack(rec[t * HH_NL + j]);
+        while (j < NR) {
+            hh_rec r = hh_rec_unpack(rec[t * NR + j]);
             uint32_t nx = hh_rec_next(j, r);
             uint32_t start = j * S + e_in, end = nx * S + r.e;
             uint32_t pe = end < c.bt ? end : c.bt;

@@ -11,7 +11,7 @@ import torch  # noqa: E402
 import huffmandecoderongpus_amd as H  # noqa: E402
 from huffmandecoderongpus_amd import synth  # noqa: E402
 
-NAMES = ["top/counter", "stage", "region", "walk", "table", "lookback", "emit", "-"]
+NAMES = ["top/counter", "stage", "region", "walk", "table", "count-lookback", "emit", "granule-wait"]
 size = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 hf, text = synth.load_source(os.path.join(ROOT, "files"))
 syn = synth.tiled_stream(hf, text, size << 20)
@@ -28,5 +28,5 @@ print(f"ms={st['ms_total']:.3f} blocks={len(cyc)} tiles={ntiles} ok={n == syn.de
 per_block = cyc.sum(1)
 print(f"cycles per block: mean {per_block.mean():.0f} max {per_block.max():.0f} -> "
       f"{per_block.mean() / (st['ms_total'] * 1e-3) / 1e9:.2f} GHz implied")
-for i, nm in enumerate(NAMES[:7]):
+for i, nm in enumerate(NAMES):
     print(f"{nm:12s} {tot[i] / ntiles:10.0f} cycles/tile  {100 * tot[i] / tot.sum():5.1f}%")
