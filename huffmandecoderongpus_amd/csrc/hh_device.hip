@@ -1,16 +1,13 @@
 // hh_device.hip -- HIP kernels (gfx950) and the device half of the C ABI.
 //
-// Fast path (O(N) memory, 64-bit offsets), three launches:
-//   k_sync  one workgroup per tile of HH_NL lane regions: tables and the
-//           tile's bits (+ halo) staged in LDS; every lane decodes its region
-//           from offset 0 (decodeallbits) and walks its exit against the next
-//           region's chain until they share a boundary (makebigtable); the
-//           tile resolves which lanes are live for each entering state and
-//           writes an HH_KM-entry transfer table.
-//   k_scan  composes the tile tables in order -> entering state and output
-//           base of every tile (calcbitsindex / findmax).
-//   k_emit  re-decodes every live run and writes its symbols through an LDS
-//           staging window with 16-byte coalesced stores (calcresult).
+// Fast path: ONE persistent launch, k_decode (O(N) memory, 64-bit offsets).
+// Tiles of HH_NR regions of S bits are dispensed in order; each workgroup
+// keeps two in flight: while it decodes tile B's regions from offset 0 with
+// boundary masks (decodeallbits) it emits tile A's runs (calcresult), then
+// walks B's region exits into their successors until the chains share a
+// boundary (makebigtable) and publishes B's transfer table.  Output bases
+// come from a decoupled look-back over those tables (calcbitsindex /
+// findmax).  C is read once from HBM, D written once.
 // Reference-shaped stage kernels (k_st_*) mirror the six .cl kernels one by
 // one for intermediate-array parity.
 #include <hip/hip_runtime.h>
@@ -28,8 +25,6 @@
 #define HH_S_MAX 320
 #define HH_SPAN_MARGIN 320        // bits beyond the last walk region
 #define HH_NW_MAX (((HH_NL + HH_KM + 1) * HH_S_MAX + HH_SPAN_MARGIN) / 32 + 4)
-#define HH_CAP (32 * 1024)        // emission staging window (bytes)
-#define HH_SCAN_T 256             // threads of the tile-scan workgroup
 #define HH_MAXLEN_FAST 256        // longest code the fast path stages for
 
 #define HIP_OK(x)                                                             \
@@ -56,20 +51,6 @@ enum { F_FAIL = 1, F_OVER = 2, F_MISMATCH = 4 };
 // ---------------------------------------------------------------------------
 // shared helpers
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void stage_tables(uint64_t *s_l1, uint32_t *s_l2, const DevTab &tab) {
-    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += blockDim.x) s_l1[i] = tab.l1[i];
-    for (uint32_t i = threadIdx.x; i < tab.l2_used; i += blockDim.x) s_l2[i] = tab.l2[i];
-}
-
-// Tile words [w0, w0+nw) of the payload; words past nwords_ok read as 0.
-__device__ __forceinline__ void stage_words(uint32_t *s_w, const uint32_t *g, uint64_t w0,
-                                            uint32_t nw, uint64_t nwords_ok) {
-    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
-        uint64_t gi = w0 + i;
-        s_w[i] = gi < nwords_ok ? __builtin_nontemporal_load(&g[gi]) : 0u;
-    }
-}
-
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -117,22 +98,6 @@ __device__ __forceinline__ uint32_t collect_exceptions(bool is_exc, uint16_t *s_
     return tot;
 }
 
-struct TileGeom {
-    uint64_t b0;       // first stream bit of the tile
-    uint32_t nw;       // staged words
-    uint32_t bt;       // stream end relative to the tile, clamped to the span
-};
-
-__device__ __forceinline__ TileGeom tile_geom(uint64_t tile, uint32_t S, uint64_t bits) {
-    TileGeom g;
-    g.b0 = tile * (uint64_t)HH_NL * S;
-    uint32_t span = (HH_NL + HH_KM + 1) * S + HH_SPAN_MARGIN;
-    g.nw = (span + 31) / 32 + 3;
-    uint64_t rem = bits - g.b0;
-    g.bt = rem < span ? (uint32_t)rem : span;
-    return g;
-}
-
 // ---------------------------------------------------------------------------
 // The fused decoder: one persistent kernel, tiles dispensed in order.
 //
@@ -146,8 +111,9 @@ __device__ __forceinline__ TileGeom tile_geom(uint64_t tile, uint32_t S, uint64_
 // out with 16-byte stores.  C is read once, D written once.
 // ---------------------------------------------------------------------------
 struct LookBack {
-    uint64_t *gran;      // [ntiles] tagged: table published + outgoing state if constant
-    uint64_t *cnt;       // [ntiles] tagged: 1 = aggregate count, 2 = inclusive prefix
+    uint64_t *gran;      // [ntiles] tagged granule: table published (+ count, state for d = 0)
+    uint64_t *incl;      // [ntiles] tagged inclusive prefix of charged counts
+    uint64_t *xst;       // [ntiles] tagged resolved outgoing state
     uint64_t *tabs;      // [ntiles][HH_KM] tile tables (sc1 stores)
     uint32_t *counter;   // tile dispenser
 };
@@ -155,7 +121,6 @@ struct LookBack {
 // 64-bit granules: the data is the flag (bits 62..63 = status, 0 = not yet).
 #define HH_ST_SHIFT 62
 #define HH_VAL_MASK ((1ull << HH_ST_SHIFT) - 1ull)
-#define HH_GR_CONST (1ull << 32)
 
 __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -168,29 +133,23 @@ enum { F_TIMEOUT = 8 };
 
 // Diagnostic build only (-DHH_STAMPS): wave 0 of every workgroup adds the
 // shader-clock cycles of each phase into dbg[block][phase].
+#define HH_NDBG 12
 #ifdef HH_STAMPS
-#define HH_NSTAMP 8
-#define STAMP_DECL uint64_t st_acc[HH_NSTAMP] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_t = __builtin_amdgcn_s_memtime();
+#define HH_NSTAMP HH_NDBG
+#define STAMP_DECL uint64_t st_acc[HH_NSTAMP] = {0}; uint64_t st_t = __builtin_amdgcn_s_memtime();
 #define STAMP(i) do { uint64_t t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_t; st_t = t_; } while (0)
 #define STAMP_FLUSH(dbg) do { if (threadIdx.x == 0) for (int i_ = 0; i_ < HH_NSTAMP; i_++) (dbg)[blockIdx.x * HH_NSTAMP + i_] = st_acc[i_]; } while (0)
+#define COUNT(i, v) do { st_acc[i] += (v); } while (0)
+#define HH_TDBG_MAX (1u << 18)
+#define TSTAMP(t, k) do { if (threadIdx.x == 0 && (t) < HH_TDBG_MAX) dbg[gridDim.x * HH_NDBG + (t) * 6 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define COUNT(i, v) do {} while (0)
+#define TSTAMP(t, k) do {} while (0)
 #define STAMP_DECL
 #define STAMP(i) do {} while (0)
 #define STAMP_FLUSH(dbg) do {} while (0)
 #endif
 #define HH_SPIN_LIMIT (1u << 22)
-
-__device__ __forceinline__ uint64_t state_pack(const hh_state &s) {
-    return (uint64_t)s.d | ((uint64_t)s.e << 8) | ((uint64_t)(uint32_t)s.delta << 32);
-}
-__device__ __forceinline__ hh_state state_unpack(uint64_t p, uint64_t base) {
-    hh_state s;
-    s.d = (uint32_t)(p & 0xff);
-    s.e = (uint32_t)((p >> 8) & 0xffffff);
-    s.delta = (int32_t)(uint32_t)(p >> 32);
-    s.base = base;
-    return s;
-}
 
 // Stage n u64 / u32 table words with all loads issued before any LDS store.
 template <uint32_t N>
@@ -201,66 +160,6 @@ __device__ __forceinline__ void stage_l1(uint64_t *dst, const uint64_t *src) {
     for (uint32_t k = 0; k < PER; k++) v[k] = src[threadIdx.x + k * HH_NL];
 #pragma unroll
     for (uint32_t k = 0; k < PER; k++) dst[threadIdx.x + k * HH_NL] = v[k];
-}
-
-__device__ __forceinline__ void stage_tile_words(uint32_t *s_w, const uint32_t *g, uint64_t w0,
-                                                 uint32_t nw, uint64_t nwords_ok) {
-    constexpr uint32_t PER = (HH_NW_MAX + HH_NL - 1) / HH_NL;
-    uint32_t v[PER];
-#pragma unroll
-    for (uint32_t k = 0; k < PER; k++) {
-        uint32_t i = threadIdx.x + k * HH_NL;
-        uint64_t gi = w0 + i;
-        v[k] = (i < nw && gi < nwords_ok) ? __builtin_nontemporal_load(&g[gi]) : 0u;
-    }
-#pragma unroll
-    for (uint32_t k = 0; k < PER; k++) {
-        uint32_t i = threadIdx.x + k * HH_NL;
-        if (i < nw) s_w[i] = v[k];
-    }
-}
-
-// Decode the run [p, pe) for output indices [o, we) into stage[idx - org]:
-// whole dwords by ds_write_b32, the partial first / last dword by bytes (the
-// neighbouring run owns its other bytes).
-__device__ __forceinline__ void emit_run_lds(const hh_ctx *c, uint32_t &p, uint32_t pe, uint64_t &o,
-                                             uint64_t we, uint8_t *stage, uint64_t org) {
-    uint32_t q = (uint32_t)(o - org);
-    while ((q & 3u) && p < pe && o < we) {
-        uint32_t s;
-        p += hh_dec1(c, p, &s);
-        stage[q++] = (uint8_t)s;
-        o++;
-    }
-    uint32_t *st32 = (uint32_t *)stage;
-    uint64_t acc = 0;
-    uint32_t nacc = 0;
-    while (p < pe && o < we) {
-        uint32_t win = hh_read32(c, p);
-        uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-        uint32_t ns = HH_L1_NSYM(e), val, n, adv;
-        if (ns && p + HH_L1_NBITS(e) <= pe && o + ns <= we) {
-            val = HH_L1_SYMS(e);
-            n = ns;
-            adv = HH_L1_NBITS(e);
-        } else {
-            uint32_t s;
-            adv = hh_dec1(c, p, &s);
-            val = s;
-            n = 1;
-        }
-        acc |= (uint64_t)val << (8u * nacc);
-        nacc += n;
-        o += n;
-        p += adv;
-        if (nacc >= 4) {
-            st32[q >> 2] = (uint32_t)acc;
-            acc >>= 32;
-            nacc -= 4;
-            q += 4;
-        }
-    }
-    for (uint32_t i = 0; i < nacc; i++) stage[q + i] = (uint8_t)(acc >> (8 * i));
 }
 
 // Poll a tagged granule until its status bits are non-zero (bounded).
@@ -286,57 +185,165 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
-// Emit the run [p, pe) to global memory at dst: dword stores, bytes for the
-// partial first / last dword (the neighbouring runs own their other bytes).
-__device__ __forceinline__ void emit_run_global(const hh_ctx *c, uint32_t p, uint32_t pe, uint8_t *dst) {
-    uintptr_t a = (uintptr_t)dst;
-    while ((a & 3u) && p < pe) {
-        uint32_t s;
-        p += hh_dec1(c, p, &s);
-        *(uint8_t *)a = (uint8_t)s;
-        a++;
-    }
-    uint64_t acc = 0;
-    uint32_t nacc = 0;
-    while (p < pe) {
-        uint32_t win = hh_read32(c, p);
-        uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-        uint32_t ns = HH_L1_NSYM(e), val, n, adv;
-        if (ns && p + HH_L1_NBITS(e) <= pe) {
-            val = HH_L1_SYMS(e);
-            n = ns;
-            adv = HH_L1_NBITS(e);
-        } else {
-            uint32_t s;
-            adv = hh_dec1(c, p, &s);
-            val = s;
-            n = 1;
-        }
-        acc |= (uint64_t)val << (8u * nacc);
-        nacc += n;
-        p += adv;
-        if (nacc >= 4) {
-            *(uint32_t *)a = (uint32_t)acc;
-            a += 4;
-            acc >>= 32;
-            nacc -= 4;
-        }
-    }
-    for (uint32_t i = 0; i < nacc; i++) *(uint8_t *)(a + i) = (uint8_t)(acc >> (8 * i));
-}
-
 // Regions per tile: the last lane decodes the NEXT tile's first region too
 // (its mask lets the tile's last walk merge without a two-pointer walk).
 #define HH_NR (HH_NL - 1)
 
+// Granule layout (gran[t], status 1 = tile t's table is published):
+//   bits  0..19 count_t(0), signed: symbols charged to the tile for d = 0
+//   bits 20..23 d_out, 24..35 e_out, 36..51 delta_out (the state for d = 0)
+//   bit  61     CONST: every entering d leads to that same outgoing state
+// Charging: count_t(d) = sum over the tile's live lanes of n + cov + delta,
+// i.e. each walk's correction is charged to the walker's tile, so a tile's
+// count depends on its predecessor only through d.  The first run of tile t
+// then starts delta_in(t) symbols before the charged prefix of tiles < t.
+#define HH_GR_PUB (1ull << 62)
+#define HH_GR_CST (1ull << 61)
+#define HH_INCL (2ull << 62)
+
+__device__ __forceinline__ uint64_t gran_pack(uint64_t xf, bool cst) {
+    return HH_GR_PUB | (cst ? HH_GR_CST : 0ull) | (uint64_t)(hh_xf_count(xf) & 0xfffffu) |
+           ((uint64_t)hh_xf_d(xf) << 20) | ((uint64_t)hh_xf_e(xf) << 24) |
+           ((uint64_t)((uint32_t)hh_xf_delta(xf) & 0xffffu) << 36);
+}
+__device__ __forceinline__ int32_t gran_cnt(uint64_t g) { return ((int32_t)((uint32_t)g << 12)) >> 12; }
+// entering-state word of the successor: d | e << 4 | delta << 16
+__device__ __forceinline__ uint64_t gran_state(uint64_t g) {
+    return ((g >> 20) & 0xfu) | (((g >> 24) & 0xfffu) << 4) | (((g >> 36) & 0xffffu) << 16);
+}
+__device__ __forceinline__ uint64_t xf_state(uint64_t xf) {
+    return (uint64_t)hh_xf_d(xf) | ((uint64_t)hh_xf_e(xf) << 4) |
+           ((uint64_t)((uint32_t)hh_xf_delta(xf) & 0xffffu) << 16);
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+    const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Charged symbols of tiles < A (A >= 1), one wave.  64 predecessors per
+// round: granule, inclusive word and the granule before it (which gives the
+// predecessor's entering d).  The nearest inclusive prefix ends the round;
+// the window's own inclusive prefixes are then published too, so later
+// look-backs stop early.  Returns false if an entering d in the window is
+// not CONST-resolvable (rare: caller takes the serial path).
+#ifdef HH_STAMPS
+#define COUNT_LB(i, v) do { lbd[i] += (v); } while (0)
+#else
+#define COUNT_LB(i, v) do {} while (0)
+#endif
+__device__ bool lookback_excl(const LookBack &lb, uint64_t A, uint32_t *flags, uint64_t *excl_out,
+                              uint32_t *nrounds, uint32_t *nspins, uint64_t *lbd) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t excl = 0;
+    int64_t top = (int64_t)A - 1;
+    int32_t c0 = 0;
+    uint32_t first0 = 64;
+    bool r0 = true;
+    for (;;) {
+        const int64_t idx = top - (int64_t)lane;
+        uint64_t iv = HH_INCL, gv = HH_GR_PUB | HH_GR_CST, gp = HH_GR_PUB | HH_GR_CST;
+        uint32_t first, spins = 0;
+        for (;;) {
+            if (idx >= 0) {
+                iv = ld_sc1(&lb.incl[idx]);
+                gv = ld_sc1(&lb.gran[idx]);
+            }
+            if (idx >= 1) gp = ld_sc1(&lb.gran[idx - 1]);
+            const uint64_t inc = __ballot((iv >> HH_ST_SHIFT) == 2);
+            first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
+            const uint64_t miss = __ballot(lane < first && ((gv >> HH_ST_SHIFT) == 0 || (gp >> HH_ST_SHIFT) == 0));
+            if (!miss) break;
+            COUNT_LB(0, __builtin_ctzll(miss));
+            COUNT_LB(1, 63 - __builtin_clzll(miss));
+            COUNT_LB(2, (__ballot(lane < first && (gv >> HH_ST_SHIFT) == 0) != 0));
+            COUNT_LB(3, first);
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > HH_SPIN_LIMIT) {
+                if (lane == 0) atomicOr(flags, (uint32_t)F_TIMEOUT);
+                *excl_out = 0;
+                return true;
+            }
+        }
+        *nrounds += 1;
+        *nspins += spins;
+        if (__ballot(lane < first && !(gp & HH_GR_CST))) return false;
+        int32_t c = 0;
+        if (lane < first) {
+            const uint32_t din = (uint32_t)(gp >> 20) & 0xfu;
+            c = din == 0 ? gran_cnt(gv) : (int32_t)hh_xf_count(ld_sc1(&lb.tabs[idx * HH_KM + din]));
+        }
+        excl += wave_sum64((uint64_t)(int64_t)c);
+        if (first < 64) excl += shfl64(iv, first) & HH_VAL_MASK;
+        if (r0) {
+            c0 = c;
+            first0 = first;
+            r0 = false;
+        }
+        if (first < 64) break;
+        top -= 64;
+    }
+    // inclusive prefixes of the first window: incl[A-1-i] = excl - sum_{j<i} c0_j
+    int32_t x = c0;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane < first0) st_sc1(&lb.incl[A - 1 - lane], ((excl - (uint64_t)(int64_t)(x - c0)) & HH_VAL_MASK) | HH_INCL);
+    *excl_out = excl;
+    return true;
+}
+
+// Tile staging: a tile's words (+ halo) are loaded to registers, then stored
+// to LDS.  Plain loads: the emission pass re-stages the same words two
+// iterations later, from L2.
+#define HH_STAGE_PER ((HH_NW_MAX + HH_NL - 1) / HH_NL)
+struct Staged {
+    uint32_t v[HH_STAGE_PER];
+};
+__device__ __forceinline__ void stage_load(Staged &s, const uint32_t *g, uint64_t w0, uint32_t nw,
+                                           uint64_t nwords_ok) {
+#pragma unroll
+    for (uint32_t k = 0; k < HH_STAGE_PER; k++) {
+        const uint32_t i = threadIdx.x + k * HH_NL;
+        const uint64_t gi = w0 + i;
+        s.v[k] = (i < nw && gi < nwords_ok) ? g[gi] : 0u;
+    }
+}
+__device__ __forceinline__ void stage_store(const Staged &s, uint32_t *dst, uint32_t nw) {
+#pragma unroll
+    for (uint32_t k = 0; k < HH_STAGE_PER; k++) {
+        const uint32_t i = threadIdx.x + k * HH_NL;
+        if (i < nw) dst[i] = s.v[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_decode: persistent; a workgroup holds three tiles.  Iteration i:
+//   (1) take tile B (dispenser) and load its bits (+ halo) into registers;
+//       re-stage the bits of tile A (taken in iteration i-2) from L2;
+//   (2) tile A: output base by look-back over its predecessors' granules.
+//       Those were published when their tiles were decoded, at least one
+//       full iteration ago, and a granule is published before its
+//       workgroup's own look-back -- so a look-back never waits on a tile
+//       whose publication itself waits (emitting one iteration after the
+//       decode instead lets waits feed on waits without bound);
+//       then A's live lanes and run offsets;
+//   (3) one loop, two independent chains per lane: B's offset-0 region
+//       decode with its boundary mask (decodeallbits) and A's run emission
+//       (calcresult), dword stores straight to HBM;
+//   (4) B's walks (makebigtable) and transfer table, published with its
+//       granule.  Then A <- P (the tile decoded in iteration i-1), P <- B.
+// C is read from HBM once (the re-stage hits L2) and D written once.
+// ---------------------------------------------------------------------------
 __global__ __launch_bounds__(HH_NL) void k_decode(const uint32_t *__restrict__ gdata, uint64_t bits,
                                                   uint64_t nwords_ok, uint32_t S, DevTab tab,
                                                   uint64_t ntiles, LookBack lb,
                                                   uint8_t *__restrict__ out, uint64_t cap,
-                                                  uint32_t *flags, uint32_t diag_stop,
-                                                  uint64_t *dbg) {
+                                                  uint32_t *flags, uint64_t *dbg) {
     __shared__ uint64_t s_l1[HH_L1_SIZE];
-    __shared__ uint32_t s_w[HH_NW_MAX];
+    __shared__ uint32_t s_w[2 * HH_NW_MAX];
     __shared__ uint32_t s_mask[HH_NL * HH_MW_MAX];
     __shared__ uint16_t s_x[HH_NL];
     __shared__ uint16_t s_n[HH_NL];
@@ -349,230 +356,290 @@ __global__ __launch_bounds__(HH_NL) void k_decode(const uint32_t *__restrict__ g
     __shared__ int32_t s_part[4][HH_KM];
     __shared__ uint64_t s_out[HH_KM];
     __shared__ uint64_t s_tab[HH_KM];
-    __shared__ uint64_t s_state[2];
+    __shared__ uint64_t s_st[2];
     __shared__ uint32_t s_tile;
     extern __shared__ uint32_t s_l2[];
 
     const uint32_t lane = threadIdx.x;
     const uint32_t mw = (S + 31) / 32;
+    const uint32_t span = (HH_NL + HH_KM + 1) * S + HH_SPAN_MARGIN;
+    const uint32_t nw = (span + 31) / 32 + 3;
     stage_l1<HH_L1_SIZE>(s_l1, tab.l1);
     for (uint32_t i = lane; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
     STAMP_DECL
 
+    // tiles A (to emit) and P (decoded last iteration): index and this
+    // lane's walk record
+    uint64_t tA = ~0ull, tP = ~0ull;
+    uint32_t aN = 0, aCov = 0, aE = 0, aK = 1;
+    int32_t aDel = 0;
+    uint32_t pN = 0, pCov = 0, pE = 0, pK = 1;
+    int32_t pDel = 0;
+    uint32_t *wB = s_w;                       // tile being decoded
+    uint32_t *wA = s_w + HH_NW_MAX;           // tile being emitted
+
     for (;;) {
         if (lane == 0) s_tile = atomicAdd(lb.counter, 1u);
-        __syncthreads();                       // also fences LDS reuse
-        const uint64_t tile = s_tile;
-        if (tile >= ntiles) break;
-        STAMP(0);
-        TileGeom g;
-        g.b0 = tile * (uint64_t)HH_NR * S;
-        {
-            const uint32_t span = (HH_NL + HH_KM + 1) * S + HH_SPAN_MARGIN;
-            g.nw = (span + 31) / 32 + 3;
-            const uint64_t rem = bits - g.b0;
-            g.bt = rem < span ? (uint32_t)rem : span;
-        }
-        stage_tile_words(s_w, gdata, g.b0 >> 5, g.nw, nwords_ok);
         __syncthreads();
-        STAMP(1);
+        const uint64_t tB = s_tile;
+        const bool hasB = tB < ntiles, hasA = tA < ntiles;
+        if (!hasA && !hasB && tP >= ntiles) break;
+        if (hasB) {
+            TSTAMP(tB, 0);
+#ifdef HH_STAMPS
+            if (lane == 0 && tB < HH_TDBG_MAX) dbg[gridDim.x * HH_NDBG + tB * 6 + 4] = blockIdx.x;
+#endif
+        }
+        uint64_t b0B = 0, b0A = 0;
+        uint32_t btB = 0, btA = 0;
+        Staged stg;
+        if (hasB) {
+            b0B = tB * (uint64_t)HH_NR * S;
+            const uint64_t rem = bits - b0B;
+            btB = rem < span ? (uint32_t)rem : span;
+            stage_load(stg, gdata, b0B >> 5, nw, nwords_ok);
+        }
+        if (hasA) {
+            b0A = tA * (uint64_t)HH_NR * S;
+            const uint64_t rem = bits - b0A;
+            btA = rem < span ? (uint32_t)rem : span;
+            Staged sa;
+            stage_load(sa, gdata, b0A >> 5, nw, nwords_ok);
+            stage_store(sa, wA, nw);
+        }
+        STAMP(0);
 
-        hh_ctx c;
-        c.w = s_w; c.sh = (uint32_t)(g.b0 & 31); c.l1 = s_l1; c.l2 = s_l2;
-        c.tree = tab.tree; c.tsym = tab.tsym; c.bt = g.bt;
+        // (2) tile A: entering state and output base
+        uint32_t pA = 0, peA = 0;
+        uintptr_t dst = 0;
+        if (hasA) {
+            TSTAMP(tA, 2);
+            if (lane < 64) {
+                uint64_t excl = 0, stw = 0;
+                bool ok = true;
+                uint32_t nrounds = 0, nspins = 0;
+                uint64_t lbd[4] = {0, 0, 0, 0};
+                if (tA > 0) ok = lookback_excl(lb, tA, flags, &excl, &nrounds, &nspins, lbd);
+                COUNT(8, lbd[0]);
+                COUNT(9, lbd[1]);
+                COUNT(10, lbd[2]);
+                COUNT(11, lbd[3]);
+                COUNT(6, nrounds + (ok ? 0ull : (1ull << 32)));
+                COUNT(7, nspins);
+                if (lane == 0) {
+                    if (tA > 0) {
+                        const uint64_t g = poll_granule(&lb.gran[tA - 1], flags);
+                        stw = (g & HH_GR_CST) ? gran_state(g) : (poll_granule(&lb.xst[tA - 1], flags) & HH_VAL_MASK);
+                        if (!ok) excl = poll_granule(&lb.incl[tA - 1], flags) & HH_VAL_MASK;
+                    }
+                    const uint64_t xf = ld_sc1(&lb.tabs[tA * HH_KM + (stw & 0xfu)]);
+                    const uint64_t incl = excl + (uint64_t)(int64_t)(int32_t)hh_xf_count(xf);
+                    st_sc1(&lb.xst[tA], xf_state(xf) | HH_GR_PUB);
+                    st_sc1(&lb.incl[tA], (incl & HH_VAL_MASK) | HH_INCL);
+                    if (tA == ntiles - 1) {
+                        flags[2] = (uint32_t)incl;
+                        flags[3] = (uint32_t)(incl >> 32);
+                    }
+                    s_st[0] = stw;
+                    s_st[1] = excl;
+                }
+            }
+            STAMP(1);
+            TSTAMP(tA, 3);
+            s_k[lane] = (uint8_t)aK;
+            __syncthreads();
+            const uint64_t sw = s_st[0];
+            const uint32_t din = (uint32_t)(sw & 0xfu);
+            s_mem[lane] = lane >= din && lane < HH_NR;
+            const uint32_t nexc = collect_exceptions(aK > 1 && lane < HH_NR, s_exc, s_cnt4);
+            if (lane == 0) {
+                for (uint32_t i = 0; i < nexc; i++) {
+                    const uint32_t j = s_exc[i], kj = s_k[j];
+                    if (!s_mem[j]) continue;
+                    for (uint32_t q = j + 1; q < j + kj && q < HH_NR; q++) s_mem[q] = 0;
+                }
+            }
+            __syncthreads();
+            const bool live = s_mem[lane] != 0;
+            if (live && lane + aK < HH_NR) {
+                s_ein[lane + aK] = (uint16_t)aE;
+                s_din[lane + aK] = (int16_t)aDel;
+            }
+            __syncthreads();
+            uint32_t e_in = 0;
+            int32_t del_in = 0;
+            if (live) {
+                e_in = lane == din ? (uint32_t)((sw >> 4) & 0xfffu) : s_ein[lane];
+                del_in = lane == din ? (int32_t)(int16_t)(uint16_t)(sw >> 16) : s_din[lane];
+            }
+            const uint32_t cnt = live ? (uint32_t)((int32_t)(aN + aCov) + del_in) : 0u;
+            uint32_t total;
+            const uint32_t off = block_excl_scan(cnt, s_cnt4, &total);
+            const uint64_t base = s_st[1] - (uint64_t)(int64_t)(int32_t)(int16_t)(uint16_t)(sw >> 16);
+            if (base + total > cap) {
+                if (lane == 0) atomicOr(flags, (uint32_t)F_OVER);
+            } else if (live) {
+                pA = lane * S + e_in;
+                const uint32_t end = (lane + aK) * S + aE;
+                peA = end < btA ? end : btA;
+                if (pA > peA) pA = peA;
+                dst = (uintptr_t)(out + base + off);
+            }
+            STAMP(2);
+        }
+        if (hasB) stage_store(stg, wB, nw);
+        __syncthreads();
 
-        // (2) region decode from offset 0 (+ boundary mask), all NL lanes
+        // (3) B's region decode + A's emission, interleaved
+        hh_ctx cA, cB;
+        cA.w = wA; cA.sh = (uint32_t)(b0A & 31); cA.l1 = s_l1; cA.l2 = s_l2; cA.tree = tab.tree; cA.tsym = tab.tsym; cA.bt = btA;
+        cB.w = wB; cB.sh = (uint32_t)(b0B & 31); cB.l1 = s_l1; cB.l2 = s_l2; cB.tree = tab.tree; cB.tsym = tab.tsym;
+        cB.bt = btB;
         const uint32_t p0 = lane * S;
-        uint32_t n = 0, x = p0;
-        {
-            struct MS {
-                uint32_t *m;
-                __device__ void operator()(uint32_t w, uint32_t v) { m[w] = v; }
-            } ms{&s_mask[lane * mw]};
-            if (p0 < c.bt) {
-                x = hh_region_count_mask(&c, p0, p0 + S, mw, &n, ms);
-            } else {
-                for (uint32_t w2 = 0; w2 < mw; w2++) s_mask[lane * mw + w2] = 0;
+        uint32_t pB = p0, limB = p0, nB = 0, mbase = p0, wdone = 0;
+        uint64_t macc = 0;
+        if (hasB && p0 < btB) limB = p0 + S < btB ? p0 + S : btB;
+        uint64_t acc = 0;
+        uint32_t nacc = 0;
+        uint32_t *msk = &s_mask[lane * mw];
+        for (;;) {
+            const bool aB = pB < limB, aA = pA < peA;
+            if (!aB && !aA) break;
+            const uint32_t qB = pB + cB.sh, qA = pA + cA.sh;
+            const uint32_t b0 = wB[qB >> 5], b1 = wB[(qB >> 5) + 1];
+            const uint32_t a0 = wA[qA >> 5], a1 = wA[(qA >> 5) + 1];
+            const uint32_t winB = __builtin_amdgcn_alignbit(b1, b0, qB & 31);
+            const uint32_t winA = __builtin_amdgcn_alignbit(a1, a0, qA & 31);
+            const uint64_t eB = s_l1[winB & (HH_L1_SIZE - 1u)];
+            const uint64_t eA = s_l1[winA & (HH_L1_SIZE - 1u)];
+            if (aB) {
+                uint32_t ns = HH_L1_NSYM(eB), l, bm = 1u;
+                if (ns && pB + HH_L1_NBITS(eB) <= limB) {
+                    l = HH_L1_NBITS(eB);
+                    bm = HH_L1_BMASK(eB);
+                } else {
+                    if (ns) {
+                        l = HH_L1_LEN0(eB);
+                    } else {
+                        uint32_t s;
+                        l = hh_escape(&cB, pB, winB, eB, &s);
+                    }
+                    ns = 1;
+                }
+                macc |= (uint64_t)bm << (pB - mbase);
+                const uint32_t rem = btB - pB;
+                pB += l < rem ? l : rem;
+                nB += ns;
+                while (pB - mbase >= 32 && wdone < mw) {
+                    msk[wdone++] = (uint32_t)macc;
+                    macc >>= 32;
+                    mbase += 32;
+                }
+            }
+            if (aA) {
+                uint32_t ns = HH_L1_NSYM(eA), val, n, adv;
+                if (ns && pA + HH_L1_NBITS(eA) <= peA) {
+                    val = HH_L1_SYMS(eA);
+                    n = ns;
+                    adv = HH_L1_NBITS(eA);
+                } else {
+                    uint32_t s;
+                    if (ns) {
+                        adv = HH_L1_LEN0(eA);
+                        s = HH_L1_SYMS(eA) & 0xffu;
+                    } else {
+                        adv = hh_escape(&cA, pA, winA, eA, &s);
+                    }
+                    if (adv > btA - pA) {
+                        s = hh_tail_symbol(&cA, pA);
+                        adv = btA - pA;
+                    }
+                    val = s;
+                    n = 1;
+                }
+                acc |= (uint64_t)val << (8u * nacc);
+                nacc += n;
+                pA += adv;
+                if (nacc >= 4) {
+                    *(uint32_t *)dst = (uint32_t)acc;   // unaligned dword store (CDNA global memory)
+                    dst += 4;
+                    acc >>= 32;
+                    nacc -= 4;
+                }
             }
         }
-        s_x[lane] = (uint16_t)(x - p0);
-        s_n[lane] = (uint16_t)n;
-        __syncthreads();
-        STAMP(2);
-        hh_rec r;
-        r.n = n; r.k = 1; r.e = 0; r.delta = 0; r.cov = 0;
-        if (lane < HH_NR) {
-            hh_masks mk = {s_mask, s_x, s_n, HH_NL, mw};
-            hh_walk_mask(&c, &mk, lane, S, x, &r);
-            r.n = n;
-            if (r.k == 0) atomicOr(flags, (uint32_t)F_FAIL);
+        for (uint32_t i = 0; i < nacc; i++) *(uint8_t *)(dst + i) = (uint8_t)(acc >> (8 * i));
+        while (wdone < mw) {
+            msk[wdone++] = (uint32_t)macc;
+            macc >>= 32;
         }
-        const uint32_t kk = r.k ? r.k : 1u;
+        s_x[lane] = (uint16_t)(pB - p0);
+        s_n[lane] = (uint16_t)nB;
+        __syncthreads();
         STAMP(3);
 
-        // (3) live regions for every entering d -> transfer table
-        s_mem[lane] = lane >= HH_NR ? 0u : (lane >= HH_KM - 1 ? 0xffu : (uint8_t)((1u << (lane + 1)) - 1u));
-        s_k[lane] = (uint8_t)kk;
-        const uint32_t nexc = collect_exceptions(kk > 1 && lane < HH_NR, s_exc, s_cnt4);
-        if (lane == 0) {
-            for (uint32_t i = 0; i < nexc; i++) {
-                uint32_t j = s_exc[i], kj = s_k[j];
-                uint8_t m = s_mem[j];
-                for (uint32_t q = j + 1; q < j + kj && q < HH_NR; q++) s_mem[q] &= (uint8_t)~m;
+        // (4) B's walks and transfer table
+        if (hasB) {
+            hh_rec r;
+            r.n = nB; r.k = 1; r.e = 0; r.delta = 0; r.cov = 0;
+            if (lane < HH_NR) {
+                hh_masks mk = {s_mask, s_x, s_n, HH_NL, mw};
+                hh_walk_mask(&cB, &mk, lane, S, pB, &r);
+                r.n = nB;
+                if (r.k == 0) atomicOr(flags, (uint32_t)F_FAIL);
             }
-        }
-        __syncthreads();
-        const uint32_t memd = s_mem[lane];
-        const int32_t contrib = (int32_t)(r.n + r.cov) + (lane + kk < HH_NR ? r.delta : 0);
-        if (lane < HH_NR && lane + kk >= HH_NR) {
-            for (uint32_t d = 0; d < HH_KM; d++)
-                if ((memd >> d) & 1u) s_out[d] = hh_xf_pack(0, r.delta, r.e, lane + kk - HH_NR);
-        }
-#pragma unroll
-        for (uint32_t d = 0; d < HH_KM; d++) {
-            int32_t v = ((memd >> d) & 1u) ? contrib : 0;
-            v = (int32_t)wave_sum((uint32_t)v);
-            if ((lane & 63) == 0) s_part[lane >> 6][d] = v;
-        }
-        __syncthreads();
-        if (lane < HH_KM) {
-            int32_t cnt = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane];
-            uint64_t o = s_out[lane];
-            s_tab[lane] = hh_xf_pack((uint32_t)cnt, hh_xf_delta(o), hh_xf_e(o), hh_xf_d(o));
-        }
-        __syncthreads();
-        STAMP(4);
-        // (4a) publish the table (sc1) and its granule: outgoing state if
-        // every entering d leads to the same one (the normal case).
-        if (lane == 0) {
-            uint64_t o0 = s_tab[0] >> 32;
-            bool cst = true;
-            for (uint32_t i = 0; i < HH_KM; i++) {
-                st_sc1(&lb.tabs[tile * HH_KM + i], s_tab[i]);
-                cst = cst && (s_tab[i] >> 32) == o0;
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint64_t o = s_tab[0];
-            uint64_t gr = (uint64_t)hh_xf_d(o) | ((uint64_t)hh_xf_e(o) << 4) |
-                          ((uint64_t)((uint32_t)hh_xf_delta(o) & 0xffffu) << 16) |
-                          (cst ? HH_GR_CONST : 0ull) | (1ull << HH_ST_SHIFT);
-            st_sc1(&lb.gran[tile], gr);
-            // (4b) entering state from the predecessor's granule
-            hh_state sin = {0, 0, 0, 0};
-            if (tile > 0) {
-                int64_t j = (int64_t)tile - 1;
-                uint64_t gj = poll_granule(&lb.gran[j], flags);
-                while (!(gj & HH_GR_CONST) && j > 0) {      // rare: walk back
-                    j--;
-                    gj = poll_granule(&lb.gran[j], flags);
-                }
-                int64_t m;
-                if (gj & HH_GR_CONST) {
-                    sin.d = (uint32_t)(gj & 0xf);
-                    sin.e = (uint32_t)((gj >> 4) & 0xfff);
-                    sin.delta = (int32_t)(int16_t)(uint16_t)(gj >> 16);
-                    m = j + 1;
-                } else {
-                    m = 0;                                   // from tile 0's entry
-                }
-                for (; m < (int64_t)tile; m++) {             // apply tables forward
-                    uint64_t v = ld_sc1(&lb.tabs[m * HH_KM + sin.d]);
-                    sin.d = hh_xf_d(v);
-                    sin.e = hh_xf_e(v);
-                    sin.delta = hh_xf_delta(v);
-                }
-            }
-            const uint64_t mycnt = (uint64_t)((int64_t)hh_xf_count(s_tab[sin.d]) + sin.delta);
-            s_state[0] = state_pack(sin);
-            s_state[1] = mycnt;
-        }
-        __syncthreads();
-        STAMP(7);
-        // (4c) output base: decoupled look-back over tagged counts, one wave
-        if (lane < 64) {
-            const uint64_t mycnt = s_state[1];
-            uint64_t excl = 0;
-            if (tile == 0) {
-                if (lane == 0) st_sc1(&lb.cnt[0], mycnt | (2ull << HH_ST_SHIFT));
-            } else {
-                if (lane == 0) st_sc1(&lb.cnt[tile], mycnt | (1ull << HH_ST_SHIFT));
-                int64_t top = (int64_t)tile - 1;
-                for (;;) {
-                    const int64_t idx = top - (int64_t)lane;
-                    uint64_t w = idx >= 0 ? ld_sc1(&lb.cnt[idx]) : (2ull << HH_ST_SHIFT);
-                    uint32_t spins = 0;
-                    uint32_t first;
-                    for (;;) {
-                        const uint32_t stv = (uint32_t)(w >> HH_ST_SHIFT);
-                        const uint64_t incl = __ballot(stv >= 2);
-                        const uint64_t zero = __ballot(stv == 0);
-                        first = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;
-                        const uint64_t rel = first < 63 ? ((2ull << first) - 1ull) : ~0ull;
-                        if (!(zero & rel)) break;
-                        if (stv == 0 && idx >= 0) w = ld_sc1(&lb.cnt[idx]);
-                        __builtin_amdgcn_s_sleep(1);
-                        if (++spins > HH_SPIN_LIMIT) {
-                            if (lane == 0) atomicOr(flags, (uint32_t)F_TIMEOUT);
-                            first = 0;
-                            w = 2ull << HH_ST_SHIFT;
-                            break;
-                        }
-                    }
-                    const uint64_t v = lane <= first ? (w & HH_VAL_MASK) : 0ull;
-                    excl += wave_sum64(v);
-                    if (first < 64) break;
-                    top -= 64;
-                }
-                if (lane == 0) st_sc1(&lb.cnt[tile], (excl + mycnt) | (2ull << HH_ST_SHIFT));
-            }
+            const uint32_t kk = r.k ? r.k : 1u;
+            STAMP(4);
+            s_mem[lane] = lane >= HH_NR ? 0u : (lane >= HH_KM - 1 ? 0xffu : (uint8_t)((1u << (lane + 1)) - 1u));
+            s_k[lane] = (uint8_t)kk;
+            const uint32_t nexc = collect_exceptions(kk > 1 && lane < HH_NR, s_exc, s_cnt4);
             if (lane == 0) {
-                if (tile == ntiles - 1) {
-                    flags[2] = (uint32_t)(excl + mycnt);
-                    flags[3] = (uint32_t)((excl + mycnt) >> 32);
+                for (uint32_t i = 0; i < nexc; i++) {
+                    const uint32_t j = s_exc[i], kj = s_k[j];
+                    const uint8_t m = s_mem[j];
+                    for (uint32_t q = j + 1; q < j + kj && q < HH_NR; q++) s_mem[q] &= (uint8_t)~m;
                 }
-                s_state[1] = excl;
             }
-        }
-        __syncthreads();
-        const hh_state sin = state_unpack(s_state[0], s_state[1]);
-        STAMP(5);
-
-        // (5) live regions of this tile and their runs, emitted to global
-        s_mem[lane] = lane >= sin.d && lane < HH_NR;
-        __syncthreads();
-        if (lane == 0) {
-            for (uint32_t i = 0; i < nexc; i++) {
-                uint32_t j = s_exc[i], kj = s_k[j];
-                if (!s_mem[j]) continue;
-                for (uint32_t q = j + 1; q < j + kj && q < HH_NR; q++) s_mem[q] = 0;
+            __syncthreads();
+            const uint32_t memd = s_mem[lane];
+            const int32_t contrib = lane < HH_NR ? (int32_t)(r.n + r.cov) + r.delta : 0;
+            if (lane < HH_NR && lane + kk >= HH_NR) {
+                for (uint32_t d = 0; d < HH_KM; d++)
+                    if ((memd >> d) & 1u) s_out[d] = hh_xf_pack(0, r.delta, r.e, lane + kk - HH_NR);
             }
+#pragma unroll
+            for (uint32_t d = 0; d < HH_KM; d++) {
+                int32_t v = ((memd >> d) & 1u) ? contrib : 0;
+                v = (int32_t)wave_sum((uint32_t)v);
+                if ((lane & 63) == 0) s_part[lane >> 6][d] = v;
+            }
+            __syncthreads();
+            if (lane < HH_KM) {
+                const int32_t cnt = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane];
+                const uint64_t o = s_out[lane];
+                s_tab[lane] = hh_xf_pack((uint32_t)cnt, hh_xf_delta(o), hh_xf_e(o), hh_xf_d(o));
+            }
+            __syncthreads();
+            if (lane == 0) {
+                const uint64_t o0 = s_tab[0] >> 32;
+                bool cst = true;
+                for (uint32_t i = 0; i < HH_KM; i++) {
+                    st_sc1(&lb.tabs[tB * HH_KM + i], s_tab[i]);
+                    cst = cst && (s_tab[i] >> 32) == o0;
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_sc1(&lb.gran[tB], gran_pack(s_tab[0], cst));
+            }
+            TSTAMP(tB, 1);
+            STAMP(5);
+            // A <- P, P <- B
+            aN = pN; aCov = pCov; aE = pE; aK = pK; aDel = pDel;
+            pN = r.n; pCov = r.cov; pE = r.e; pK = kk; pDel = r.delta;
+        } else {
+            aN = pN; aCov = pCov; aE = pE; aK = pK; aDel = pDel;
         }
-        __syncthreads();
-        const bool live = s_mem[lane] != 0;
-        if (live && lane + kk < HH_NR) {
-            s_ein[lane + kk] = (uint16_t)r.e;
-            s_din[lane + kk] = (int16_t)r.delta;
-        }
-        __syncthreads();
-        uint32_t e_in = 0;
-        int32_t del_in = 0;
-        if (live) {
-            e_in = lane == sin.d ? sin.e : s_ein[lane];
-            del_in = lane == sin.d ? sin.delta : s_din[lane];
-        }
-        const uint32_t cnt = live ? (uint32_t)((int32_t)(r.n + r.cov) + del_in) : 0u;
-        uint32_t total;
-        const uint32_t off = block_excl_scan(cnt, s_cnt4, &total);
-        const uint64_t base = sin.base;
-        if (base + total > cap) {
-            if (lane == 0) atomicOr(flags, (uint32_t)F_OVER);
-        } else if (live) {
-            const uint32_t start = lane * S + e_in;
-            const uint32_t end = (lane + kk) * S + r.e;
-            const uint32_t pe = end < c.bt ? end : c.bt;
-            if (start < pe) emit_run_global(&c, start, pe, out + base + off);
-        }
-        STAMP(6);
+        tA = tP;
+        tP = hasB ? tB : ~0ull;
     }
     STAMP_FLUSH(dbg);
 }
@@ -686,7 +753,6 @@ struct hh_decoder {
     hh_stats stats;
     uint32_t grid;       // persistent grid size (occupancy x CUs)
     size_t grid_l2b;     // dynamic LDS the grid was sized for
-    uint32_t diag_stop;  // HIPHUFF_DIAG_STOP: time the phases (diagnostic only)
     uint64_t *d_dbg;     // per-block phase cycles (HH_STAMPS builds)
 };
 
@@ -726,8 +792,6 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
         return HH_ERR_DEVICE;
     }
     for (int i = 0; i < 4; i++) hipEventCreate(&d->ev[i]);
-    const char *ds = getenv("HIPHUFF_DIAG_STOP");
-    d->diag_stop = ds ? (uint32_t)atoi(ds) : 0u;
     *out = d;
     return HH_OK;
 }
@@ -818,8 +882,8 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     const uint64_t tb = (uint64_t)HH_NR * S;
     const uint64_t ntiles = (bits + tb - 1) / tb;
     const uint64_t nwords_ok = ((bits + 7) / 8 + HH_PAYLOAD_PAD) / 4;
-    // workspace: [flags 64 B | counter, granules, counts (zeroed) | tables]
-    const size_t zero_bytes = (16 + ntiles * 16 + 15) & ~(size_t)15;
+    // workspace: [flags 64 B | counter, gran, incl, xst (zeroed) | tables]
+    const size_t zero_bytes = (16 + ntiles * 24 + 15) & ~(size_t)15;
     size_t need = 64 + zero_bytes + ntiles * HH_KM * 8 + 256;
     int rc = ensure_ws(d, need);
     if (rc) return rc;
@@ -828,7 +892,8 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     LookBack lb;
     lb.counter = (uint32_t *)(w + 64);
     lb.gran = (uint64_t *)(w + 64 + 16);
-    lb.cnt = lb.gran + ntiles;
+    lb.incl = lb.gran + ntiles;
+    lb.xst = lb.incl + ntiles;
     lb.tabs = (uint64_t *)(w + 64 + zero_bytes);
     const size_t l2b = sizeof(uint32_t) * d->tab.l2_used;
     if (!d->grid || d->grid_l2b != l2b) {
@@ -838,16 +903,19 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
         if (d->d_dbg) HIP_OK(hipFree(d->d_dbg));
         HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
         d->grid = (uint32_t)((per_cu > 0 ? per_cu : 1) * ncu);
-        HIP_OK(hipMalloc(&d->d_dbg, (size_t)d->grid * 8 * sizeof(uint64_t)));
-        HIP_OK(hipMemset(d->d_dbg, 0, (size_t)d->grid * 8 * sizeof(uint64_t)));
+        size_t dbg_words = (size_t)d->grid * HH_NDBG;
+#ifdef HH_STAMPS
+        dbg_words += (size_t)HH_TDBG_MAX * 6;
+#endif
+        HIP_OK(hipMalloc(&d->d_dbg, dbg_words * sizeof(uint64_t)));
+        HIP_OK(hipMemset(d->d_dbg, 0, dbg_words * sizeof(uint64_t)));
     }
     const uint32_t grid = (uint32_t)(ntiles < d->grid ? ntiles : d->grid);
 
     HIP_OK(hipMemsetAsync(d_flags, 0, 64 + zero_bytes, st));
     HIP_OK(hipEventRecord(d->ev[0], st));
     hipLaunchKernelGGL(k_decode, dim3(grid), dim3(HH_NL), l2b, st, (const uint32_t *)d_data, bits,
-                       nwords_ok, S, d->tab, ntiles, lb, (uint8_t *)d_out, cap, d_flags, d->diag_stop,
-                       d->d_dbg);
+                       nwords_ok, S, d->tab, ntiles, lb, (uint8_t *)d_out, cap, d_flags, d->d_dbg);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d->ev[1], st));
     HIP_OK(hipMemcpyAsync(d->h_flags, d_flags, 16, hipMemcpyDeviceToHost, st));
@@ -862,7 +930,6 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     d->stats.ms_emit = ms;
     d->stats.lanes = ntiles * HH_NR;
     d->stats.out_len = total;
-    if (d->diag_stop) { *out_len = 0; return HH_OK; }
     if (fl & F_TIMEOUT) return HH_ERR_TIMEOUT;
     if (fl & F_FAIL) {
         // A walk found no shared boundary within HH_KM regions: the code does
@@ -1037,10 +1104,26 @@ extern "C" int hh_stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits
 
 // Diagnostic: per-block phase cycle sums of the last decode (HH_STAMPS
 // builds; zeros otherwise).  Returns the number of blocks written.
+// Diagnostic builds only: per-tile global timestamps (s_memrealtime, 100 MHz)
+// [grab, granule published, look-back start, look-back end, block, -].
+extern "C" int hh_debug_tile_times(hh_decoder *d, uint64_t *out, int max_tiles) {
+#ifdef HH_STAMPS
+    if (!d || !out || !d->d_dbg) return 0;
+    int n = max_tiles < (int)HH_TDBG_MAX ? max_tiles : (int)HH_TDBG_MAX;
+    if (hipMemcpy(out, d->d_dbg + (size_t)d->grid * HH_NDBG, (size_t)n * 6 * sizeof(uint64_t),
+                  hipMemcpyDeviceToHost) != hipSuccess)
+        return 0;
+    return n;
+#else
+    (void)d; (void)out; (void)max_tiles;
+    return 0;
+#endif
+}
+
 extern "C" int hh_debug_phase_cycles(hh_decoder *d, uint64_t *out, int max_blocks) {
     if (!d || !out || !d->d_dbg) return 0;
     int n = (int)d->grid < max_blocks ? (int)d->grid : max_blocks;
-    if (hipMemcpy(out, d->d_dbg, (size_t)n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(out, d->d_dbg, (size_t)n * HH_NDBG * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         return HH_ERR_DEVICE;
     return n;
 }

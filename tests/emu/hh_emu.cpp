@@ -3,7 +3,8 @@
 // Runs the kernel's per-lane building blocks (hh_algo.h) on host arrays with
 // the kernel's geometry -- tiles of HH_NL-1 regions, one auxiliary lane that
 // decodes the next tile's first region, boundary masks, mask walks, tile
-// transfer tables, ordered state application, emission -- so the stitching
+// transfer tables, ordered state application, the look-back's charged
+// counts, emission -- so the stitching
 // logic is checked against the oracle without a GPU.  Every lane's mask walk
 // is also cross-checked against the plain two-pointer walk.  Nothing in the
 // product links this file; it builds into tests/emu/libhh_emu.so.
@@ -111,6 +112,22 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
     for (uint64_t t = 0; t < ntiles; t++) st[t + 1] = hh_xf_apply(&tab[t * HH_KM], st[t]);
     uint64_t total = st[ntiles].base;
     if (total > cap) return HH_ERR_CAPACITY;
+
+    // The kernel's look-back sums CHARGED counts (each walk's delta charged
+    // to the walker's tile: count_t(d) = sum over live lanes of n+cov+delta)
+    // and starts tile t's first run delta_in(t) symbols before that prefix.
+    {
+        int64_t charged = 0;
+        for (uint64_t t = 0; t < ntiles; t++) {
+            if ((int64_t)st[t].base != charged - st[t].delta) return HH_ERR_INTERNAL - 200;
+            for (uint32_t j = st[t].d; j < NR;) {
+                hh_rec r = hh_rec_unpack(rec[t * NR + j]);
+                charged += (int64_t)r.n + r.cov + r.delta;
+                j = hh_rec_next(j, r);
+            }
+        }
+        if (charged != (int64_t)total) return HH_ERR_INTERNAL - 201;
+    }
 
     struct Sink {
         uint8_t *out;
