@@ -104,7 +104,6 @@ _SIGS = {
                            C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
     "hipHuffApproach": ([C.c_void_p, C.c_void_p, C.c_void_p], None),
     "hh_debug_phase_cycles": ([C.c_void_p, C.c_void_p, C.c_int], C.c_int),
-    "hh_debug_tile_times": ([C.c_void_p, C.c_void_p, C.c_int], C.c_int),
 }
 
 
@@ -247,13 +246,6 @@ class Decoder:
         """Diagnostic (HH_STAMPS builds): per-block cycles of each phase."""
         buf = np.zeros((max_blocks, 12), np.uint64)
         n = lib().hh_debug_phase_cycles(self._h, buf.ctypes.data, max_blocks)
-        return buf[: max(n, 0)]
-
-    def tile_times(self, max_tiles: int = 1 << 18) -> np.ndarray:
-        """Diagnostic (HH_STAMPS builds): per-tile s_memrealtime stamps
-        [grab, granule published, look-back start, look-back end, block, -]."""
-        buf = np.zeros((max_tiles, 6), np.uint64)
-        n = lib().hh_debug_tile_times(self._h, buf.ctypes.data, max_tiles)
         return buf[: max(n, 0)]
 
     def decode_host(self, payload: np.ndarray, bits: int, cap: int) -> np.ndarray:

@@ -1,29 +1,39 @@
 /*
  * hh_algo.h -- per-lane building blocks of the O(N) speculative decoder.
  *
- * Everything here is __host__ __device__: the HIP kernels (hh_device.hip)
- * call it on LDS-resident data, and the test-only emulator
- * (tests/emu/hh_emu.cpp) calls it on host arrays to check the stitching
- * logic against the oracle without a GPU.
+ * Everything here is __host__ __device__: the HIP kernel (hh_device.hip)
+ * calls it on LDS-resident data, and the test-only emulator
+ * (tests/emu/hh_emu.cpp) calls it on host arrays with the kernel's exact
+ * tile geometry and LDS layout, so the stitching logic is checked against
+ * the oracle without a GPU.
  *
  * Restatement of the reference pipeline (ReleaseCL/kernels/ *.cl):
  *
- *  decodeallbits  -> a lane decodes its region of S bits speculatively from
- *                    the region start (offset 0): `hh_region_count`.
+ *  decodeallbits  -> lane j decodes its region of S bits speculatively from
+ *                    the region start R_j (offset 0): n_j symbols start in
+ *                    the region, x_j is the chain's first position at or
+ *                    past the region end (`hh_region_count`).
  *  makebigtable   -> instead of pointer doubling over an int32[25][bits]
- *                    table, chains are stitched directly: the chain leaving
- *                    region j (exact if region j's own chain is exact at its
- *                    exit) is walked in lock-step with region j+1's
- *                    offset-0 chain until the two share a code boundary
- *                    (`hh_walk`).  Sharing a boundary means identical from
- *                    there on, so the merge is exact, never a heuristic.  A
- *                    walk that finds no shared boundary in region j+1 carries
- *                    on into j+2, ... (region j+1 is then "covered").
- *  calcbitsindex  -> the output index of every true boundary follows from a
- *                    prefix sum over per-region symbol counts (hh_orbit_*).
- *  calcresult     -> emission: each live region re-decodes its exact run and
- *                    writes the symbols (`hh_emit_run`).
+ *                    table, each region exit is walked against the next
+ *                    region's offset-0 chain, two pointers, until the chains
+ *                    share a code boundary (`hh_walk`).  A shared boundary
+ *                    means identical chains from there on, so the merge is
+ *                    exact, never a heuristic.  delta_j = (walk symbols
+ *                    before the merge) - (region j+1's own symbols before it).
+ *  calcbitsindex  -> output index of every true boundary: prefix sum of the
+ *                    CHARGED counts c_j = n_j + delta_j.  The true chain has
+ *                    n_j + delta_{j-1} symbols in region j, so the charged
+ *                    sum of a tile does not depend on the tile's entry and
+ *                    the cross-tile scan is a plain sum.
+ *  calcresult     -> each lane re-decodes the exact run [x_{j-1}, x_j) and
+ *                    writes its symbols (`hh_emit_step`).
  *  findmax        -> the total of the prefix sum.
+ *
+ * Chain semantics follow decodeallbits.cl:10-33: from position p, a code of
+ * length l ends at p + l; a code cut off by the end of the stream (p + l >
+ * bt) is the last symbol, its byte is the sym of the tree node the walk
+ * reached (the tail rule), and the chain ends at bt.  Positions are
+ * therefore clamped to bt.
  */
 #ifndef HH_ALGO_H_
 #define HH_ALGO_H_
@@ -38,35 +48,78 @@
 #endif
 /* This header is C++ (hipcc for the kernels, g++ for the test emulator). */
 
-/* Lanes per tile, max regions a walk may cross (the cross-tile state d is
- * in [0, HH_KM)). */
-#define HH_NL 256
-#define HH_KM 8
+/* ------------------------------------------------------------------ */
+/* Tile geometry.                                                       */
+/*   HH_NL lanes per tile (one workgroup), lane j owns region j of S     */
+/*   bits.  A walk may cross up to HH_KM regions before it merges (runs */
+/*   of a repeated symbol keep chains apart for hundreds of bits), so   */
+/*   the tile stages HH_KM regions of the next tile too, plus a halo     */
+/*   for codes running past the last one.                                */
+/*   The bitstream is staged in LDS TRANSPOSED: tile word g lives at     */
+/*   (g % sw) * HH_NLS + g / sw, i.e. region r is column r.  Lanes read  */
+/*   their own columns, so a wave's reads fall in distinct banks         */
+/*   (HH_NLS is a multiple of 32) however far apart the lanes' chains    */
+/*   are.                                                                */
+/* ------------------------------------------------------------------ */
+#define HH_NL 512
+#define HH_NR HH_NL           /* regions per tile */
+#define HH_KM 8               /* max regions one walk may cross */
+#define HH_NCOL (HH_NR + HH_KM + 1)   /* staged columns */
+#define HH_NLS 544            /* >= HH_NCOL, multiple of 32 */
+#define HH_SW_MAX 12          /* max words per region (S <= 384) */
+#define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
+                                 as a failed walk) */
+
+HH_HD uint32_t hh_umulhi(uint32_t a, uint32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umulhi(a, b);
+#else
+    return (uint32_t)(((uint64_t)a * b) >> 32);
+#endif
+}
+
+HH_HD uint32_t hh_ctz(uint32_t v) {   /* v != 0 */
+    return (uint32_t)__builtin_ctz(v);
+}
+HH_HD uint32_t hh_popc(uint32_t v) { return (uint32_t)__builtin_popcount(v); }
+HH_HD uint32_t hh_lowmask(uint32_t o) { return o >= 32 ? 0xffffffffu : ((1u << o) - 1u); }
+
+/* ceil(2^32 / sw): hh_umulhi(g, magic) == g / sw exactly for g < 2^20. */
+HH_HD uint32_t hh_magic(uint32_t sw) { return (uint32_t)((0x100000000ull + sw - 1) / sw); }
 
 typedef struct {
-    const uint32_t *w;      /* tile words; stream bit (tile_bit0 + p) is bit
-                               ((p + sh) & 31) of w[(p + sh) >> 5]         */
-    uint32_t sh;            /* tile_bit0 & 31                              */
-    const uint64_t *l1;     /* HH_L1_SIZE entries                          */
+    const uint32_t *w;    /* transposed tile words                        */
+    uint32_t sw;          /* words per region                             */
+    uint32_t magic;       /* hh_magic(sw)                                 */
+    const uint64_t *l1;   /* HH_L1_SIZE entries                           */
     const uint32_t *l2;
-    const uint32_t *tree;   /* compact tree                                */
+    const uint32_t *tree; /* compact tree (tail symbols, very long codes) */
     const uint8_t *tsym;
-    uint32_t bt;            /* end of stream relative to the tile (clamped) */
+    uint32_t bt;          /* end of stream relative to the tile (clamped) */
 } hh_ctx;
 
-HH_HD uint32_t hh_read32(const hh_ctx *c, uint32_t p) {
-    uint32_t q = p + c->sh;
-    uint32_t lo = c->w[q >> 5], hi = c->w[(q >> 5) + 1];
+/* The kernel is instantiated per words-per-region (the kernel's hh_ctx has
+ * a compile-time sw), so this division folds to shifts / a multiply-high. */
+HH_HD uint32_t hh_word(const hh_ctx *c, uint32_t g) {
+    uint32_t r = g / c->sw;
+    uint32_t k = g - r * c->sw;
+    return c->w[k * HH_NLS + r];
+}
+
+/* 32 stream bits from tile position p, stream bit p in bit 0 (LSB-first
+ * bytes: the reference's window convention, linapproach.c:207-209). */
+HH_HD uint32_t hh_win(const hh_ctx *c, uint32_t p) {
+    uint32_t g = p >> 5;
+    uint32_t lo = hh_word(c, g), hi = hh_word(c, g + 1);
 #if defined(__HIP_DEVICE_COMPILE__)
-    return __builtin_amdgcn_alignbit(hi, lo, q & 31);
+    return __builtin_amdgcn_alignbit(hi, lo, p & 31);
 #else
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (q & 31));
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (p & 31));
 #endif
 }
 
 HH_HD uint32_t hh_bit(const hh_ctx *c, uint32_t p) {
-    uint32_t q = p + c->sh;
-    return (c->w[q >> 5] >> (q & 31)) & 1u;
+    return (hh_word(c, p >> 5) >> (p & 31)) & 1u;
 }
 
 /* The reference's tail rule (decodeallbits.cl:20-31): walking from the root
@@ -84,9 +137,8 @@ HH_HD uint32_t hh_tail_symbol(const hh_ctx *c, uint32_t p) {
 }
 
 /* First code longer than HH_P bits: second-level table, then (very long
- * codes only) a bit-serial walk.  Returns the code length; a walk that hits
- * the end of the stream returns the cut-off length with the internal
- * node's symbol, exactly the tail rule. */
+ * codes only) a bit-serial walk.  Returns the code length.  A walk that
+ * hits the end of the stream returns the cut-off length. */
 HH_HD uint32_t hh_escape(const hh_ctx *c, uint32_t p, uint32_t win, uint64_t e,
                          uint32_t *sym) {
     uint32_t q = HH_L1_L2Q(e), base = HH_L1_L2BASE(e);
@@ -105,423 +157,198 @@ HH_HD uint32_t hh_escape(const hh_ctx *c, uint32_t p, uint32_t win, uint64_t e,
     }
 }
 
-/* Length of the one code starting at p (< bt), cut at the stream end. */
-HH_HD uint32_t hh_len1(const hh_ctx *c, uint32_t p) {
-    uint32_t win = hh_read32(c, p);
+/* One table lookup at p: up to HH_K whole symbols.
+ *   nb   bits of those symbols (next lookup starts at p + nb)
+ *   ns   symbols, bm their start offsets (bit 0 always set)
+ *   len0 length of the first symbol, syms the bytes (first in bits 0..7) */
+typedef struct {
+    uint32_t nb, ns, bm, len0, syms;
+} hh_look;
+
+HH_HD hh_look hh_lookup(const hh_ctx *c, uint32_t p) {
+    uint32_t win = hh_win(c, p);
     uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-    uint32_t l;
-    if (HH_L1_NSYM(e)) {
-        l = HH_L1_LEN0(e);
+    hh_look L;
+    L.ns = HH_L1_NSYM(e);
+    if (L.ns) {
+        L.nb = HH_L1_NBITS(e);
+        L.bm = HH_L1_BMASK(e);
+        L.len0 = HH_L1_LEN0(e);
+        L.syms = HH_L1_SYMS(e);
     } else {
         uint32_t s;
-        l = hh_escape(c, p, win, e, &s);
+        L.nb = L.len0 = hh_escape(c, p, win, e, &s);
+        L.ns = 1;
+        L.bm = 1;
+        L.syms = s;
     }
-    uint32_t rem = c->bt - p;
-    return l < rem ? l : rem;
+    return L;
 }
 
-/* One symbol at p (< bt) with its length (tail rule applied). */
-HH_HD uint32_t hh_dec1(const hh_ctx *c, uint32_t p, uint32_t *sym) {
-    uint32_t win = hh_read32(c, p);
-    uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-    uint32_t l, s;
-    if (HH_L1_NSYM(e)) {
-        l = HH_L1_LEN0(e);
-        s = HH_L1_SYMS(e) & 0xffu;
-    } else {
-        l = hh_escape(c, p, win, e, &s);
-    }
-    if (l > c->bt - p) {
-        s = hh_tail_symbol(c, p);
-        l = c->bt - p;
-    }
-    *sym = s;
-    return l;
+/* Offset of the lookup's first boundary at or after offset d (>= 1): a
+ * symbol start inside the lookup, or nb (the next lookup's start). */
+HH_HD uint32_t hh_first_ge(const hh_look &L, uint32_t d) {
+    uint32_t m = d < 32 ? L.bm & ~hh_lowmask(d) : 0u;
+    return m ? hh_ctz(m) : L.nb;
 }
+/* Symbols of the lookup that start before offset o. */
+HH_HD uint32_t hh_syms_before(const hh_look &L, uint32_t o) { return hh_popc(L.bm & hh_lowmask(o)); }
 
-/* Phase A (decodeallbits restated): count the symbols of the chain that
- * starts at p0 and whose starts lie in [p0, lim).  Returns the exit, the
- * first position >= lim on the chain (or bt). */
-HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim,
-                               uint32_t *count) {
+/* Pass 1 (decodeallbits restated): the chain from p0 (< lim), counting the
+ * symbols that start in [p0, lim) (lim <= bt).  Returns the exit: the
+ * chain's first position >= lim (bt if the stream ends first). */
+HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint32_t *count) {
     uint32_t p = p0, n = 0;
-    if (lim > c->bt) lim = c->bt;
     while (p < lim) {
-        uint32_t win = hh_read32(c, p);
-        uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-        uint32_t ns = HH_L1_NSYM(e);
-        uint32_t l;
-        if (ns) {
-            uint32_t nb = HH_L1_NBITS(e);
-            if (p + nb <= lim) {
-                p += nb;
-                n += ns;
-                continue;
-            }
-            l = HH_L1_LEN0(e);
-        } else {
-            uint32_t s;
-            l = hh_escape(c, p, win, e, &s);
-        }
-        uint32_t rem = c->bt - p;
-        p += l < rem ? l : rem;
-        n += 1;
+        hh_look L = hh_lookup(c, p);
+        uint32_t o = hh_first_ge(L, lim - p);
+        n += hh_syms_before(L, o);
+        p += o;
     }
     *count = n;
-    return p;
+    return p < c->bt ? p : c->bt;
 }
 
-/* Walk result, packed per lane (u64):
- *   bits  0..15 n      symbols of the lane's own offset-0 chain in its region
- *   bits 16..31 cov    symbols of the walk in covered regions (k > 1)
- *   bits 32..47 delta  (signed) correction for the region the walk merged in:
- *                      walk symbols before the merge minus that region's own
- *                      chain symbols before the merge
- *   bits 48..59 e      entry offset of the walk into the merge region
- *   bits 60..63 k      regions crossed (1 = merged in the next region);
- *                      0 = failed (no merge within HH_KM regions)
- */
+/* Pass 2 (makebigtable restated): the chain W leaving region j at x (its
+ * exit) walked against the offset-0 chain C of region j+1, two pointers: the
+ * one behind moves to its first boundary at or past min(other, region end).
+ * Equal positions = merged.  Both at/past the region end without meeting =
+ * region j+1 is COVERED by W; W (now at its first boundary past that
+ * region's start) carries on against region j+2's chain, and so on, up to
+ * HH_KM regions.  Any common boundary is a valid merge point: after it the
+ * chains are identical, so counts taken there are exact.
+ *   k     regions crossed (1 = merged in region j+1), 0 = no merge
+ *   e     W's first boundary in the merge region, as an offset from its start
+ *   cov   W's symbols from x up to that boundary (the covered regions)
+ *   delta W's symbols from there to the merge minus C's symbols before it */
 typedef struct {
-    uint32_t n, cov, e, k;
+    uint32_t k, e, cov;
     int32_t delta;
-} hh_rec;
+} hh_wk;
 
-HH_HD uint64_t hh_rec_pack(hh_rec r) {
-    return (uint64_t)(r.n & 0xffffu) | ((uint64_t)(r.cov & 0xffffu) << 16) |
-           ((uint64_t)((uint32_t)r.delta & 0xffffu) << 32) |
-           ((uint64_t)(r.e & 0xfffu) << 48) | ((uint64_t)(r.k & 0xfu) << 60);
-}
-HH_HD hh_rec hh_rec_unpack(uint64_t v) {
-    hh_rec r;
-    r.n = (uint32_t)(v & 0xffffu);
-    r.cov = (uint32_t)((v >> 16) & 0xffffu);
-    r.delta = (int32_t)(int16_t)(uint16_t)((v >> 32) & 0xffffu);
-    r.e = (uint32_t)((v >> 48) & 0xfffu);
-    r.k = (uint32_t)(v >> 60);
-    return r;
-}
-
-/* Phase B (makebigtable restated): the chain leaving region `lane` at x
- * (>= region end, <= bt) walked against region lane+1's offset-0 chain,
- * two pointers, always advancing the one behind; a pointer that has left
- * the region stops.  Same position = merged.  Both out of the region and
- * different = region lane+1 is covered by this walk; continue with the next
- * region.  S = region bits. */
-HH_HD void hh_walk(const hh_ctx *c, uint32_t lane, uint32_t S, uint32_t x,
-                   hh_rec *r) {
-    r->k = 1; r->e = 0; r->delta = 0; r->cov = 0;
-    uint32_t A = x;
-    uint32_t R = lane + 1;
-    if (A < R * S) return;      /* stream ended inside this region */
-    for (uint32_t it = 0; it < HH_KM; it++, R++) {
-        uint32_t Lr = R * S, Le = Lr + S;
-        uint32_t eA = A - Lr;
-        uint32_t B = Lr, ca = 0, cb = 0;
-        for (;;) {
+HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x) {
+    hh_wk r = {0u, 0u, 0u, 0};
+    const uint32_t bt = c->bt;
+    uint32_t A = x < bt ? x : bt;
+    int32_t ca = 0;
+    uint32_t it = 0;
+    for (uint32_t k = 1; k <= HH_KM; k++) {
+        const uint32_t R = (j + k) * S;
+        const uint32_t Ec = R + S < bt ? R + S : bt;
+        const int32_t ca0 = ca;
+        const uint32_t e = A > R ? A - R : 0u;   /* A == bt <= R: stream ended */
+        uint32_t B = R < bt ? R : bt;
+        int32_t cb = 0;
+        for (; it < HH_WALK_MAX; it++) {
             if (A == B) {
-                r->k = it + 1;
-                r->e = eA;
-                r->delta = (int32_t)ca - (int32_t)cb;
-                return;
+                r.k = k;
+                r.e = e;
+                r.cov = (uint32_t)ca0;
+                r.delta = (ca - ca0) - cb;
+                return r;
             }
-            uint32_t ad = A >= Le, bd = B >= Le;
-            if (ad && bd) break;
-            if (!ad && (bd || A < B)) {
-                A += hh_len1(c, A);
-                ca++;
-            } else {
-                B += hh_len1(c, B);
-                cb++;
-            }
+            const bool mvA = A < B;
+            const uint32_t P = mvA ? A : B, Q = mvA ? B : A;
+            if (P >= Ec) break;                  /* both past the region end */
+            const uint32_t tgt = Q < Ec ? Q : Ec;
+            hh_look L = hh_lookup(c, P);
+            const uint32_t o = hh_first_ge(L, tgt - P);
+            const int32_t n = (int32_t)hh_syms_before(L, o);
+            uint32_t np = P + o;
+            if (np > bt) np = bt;
+            if (mvA) { A = np; ca += n; } else { B = np; cb += n; }
         }
-        r->cov += ca;
+        if (it >= HH_WALK_MAX) break;
     }
-    r->k = 0;   /* no merge within HH_KM regions */
+    return r;   /* k == 0: failed */
 }
 
 /* ------------------------------------------------------------------ */
-/* Boundary masks.  Phase A also records, for its region, a bit per     */
-/* position that starts a code of its offset-0 chain (mask word w, bit  */
-/* i <=> position 32w + i of the region).  A walk then decodes only the */
-/* incoming chain, several codes per lookup, and tests each lookup's    */
-/* start positions against the next region's mask -- the first common   */
-/* start is exactly the two-pointer merge point (hh_walk), found in a   */
-/* fraction of the steps.                                               */
+/* Tile transfer table.  The state entering a tile is (d, e, delta):    */
+/* regions 0..d-1 are covered by the previous tile's last walk, the     */
+/* first live region d is entered e bits past its start, and delta is   */
+/* that walk's correction.  Lane j is live for entering d iff d <= j    */
+/* and no live walk covers it; its charged count is n + cov + delta.    */
+/* For every d in [0, HH_KM) the table gives the charged count of the   */
+/* tile's live lanes and the state leaving the tile (from its last live */
+/* lane, the one whose walk crosses the tile end).                      */
 /* ------------------------------------------------------------------ */
-#define HH_MW_MAX 10   /* mask words per region (S <= 320) */
-
-typedef struct {
-    const uint32_t *m;    /* [nreg][mw] region masks            */
-    const uint16_t *x;    /* [nreg] exit offset from region start */
-    const uint16_t *n;    /* [nreg] own-chain symbol counts        */
-    uint32_t nreg;        /* regions with a mask (tile-local 0..)  */
-    uint32_t mw;          /* words per region mask                 */
-} hh_masks;
-
-/* Phase A with the boundary mask: like hh_region_count, plus
- * sink(w, word) for every mask word w in [0, mw). */
-template <class MaskSink>
-HH_HD uint32_t hh_region_count_mask(const hh_ctx *c, uint32_t p0, uint32_t lim, uint32_t mw,
-                                    uint32_t *count, MaskSink &sink) {
-    uint32_t p = p0, n = 0, wdone = 0, mbase = p0;
-    uint64_t macc = 0;
-    if (lim > c->bt) lim = c->bt;
-    while (p < lim) {
-        uint32_t win = hh_read32(c, p);
-        uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-        uint32_t ns = HH_L1_NSYM(e);
-        uint32_t l, bm = 1u;
-        if (ns) {
-            uint32_t nb = HH_L1_NBITS(e);
-            if (p + nb <= lim) {
-                l = nb;
-                bm = HH_L1_BMASK(e);
-            } else {
-                l = HH_L1_LEN0(e);
-                ns = 1;
-            }
-        } else {
-            uint32_t s;
-            l = hh_escape(c, p, win, e, &s);
-            ns = 1;
-        }
-        macc |= (uint64_t)bm << (p - mbase);
-        uint32_t rem = c->bt - p;
-        p += l < rem ? l : rem;
-        n += ns;
-        while (p - mbase >= 32 && wdone < mw) {
-            sink(wdone++, (uint32_t)macc);
-            macc >>= 32;
-            mbase += 32;
-        }
-    }
-    while (wdone < mw) {
-        sink(wdone++, (uint32_t)macc);
-        macc >>= 32;
-    }
-    *count = n;
-    return p;
+#define HH_DEL_BITS 10
+HH_HD uint32_t hh_state_pack(uint32_t d, uint32_t e, int32_t delta) {
+    return (d & 0xfu) | ((e & 0x7fu) << 4) | (((uint32_t)delta & ((1u << HH_DEL_BITS) - 1u)) << 11);
 }
-
-/* Symbols of region r's own chain that start before region offset `off`. */
-HH_HD uint32_t hh_mask_rank(const hh_masks *mk, uint32_t r, uint32_t off) {
-    const uint32_t *m = mk->m + r * mk->mw;
-    uint32_t cnt = 0, w = 0;
-    for (; w < (off >> 5); w++) cnt += __builtin_popcount(m[w]);
-    if (off & 31u) cnt += __builtin_popcount(m[w] & ((1u << (off & 31u)) - 1u));
-    return cnt;
+HH_HD uint32_t hh_state_d(uint32_t s) { return s & 0xfu; }
+HH_HD uint32_t hh_state_e(uint32_t s) { return (s >> 4) & 0x7fu; }
+HH_HD int32_t hh_state_delta(uint32_t s) {
+    return (int32_t)(s << (32 - 11 - HH_DEL_BITS)) >> (32 - HH_DEL_BITS);
 }
+/* table entry: charged count (signed 20 bits) | state << 20 */
+HH_HD uint64_t hh_tab_pack(int32_t count, uint32_t state) {
+    return (uint64_t)((uint32_t)count & 0xfffffu) | ((uint64_t)state << 20);
+}
+HH_HD int32_t hh_tab_count(uint64_t v) { return (int32_t)((uint32_t)v << 12) >> 12; }
+HH_HD uint32_t hh_tab_state(uint64_t v) { return (uint32_t)(v >> 20) & 0x1fffffu; }
 
-/* Phase B with masks: same result as hh_walk.  Regions >= mk->nreg (past
- * the tile's masks) fall back to the two-pointer walk. */
-HH_HD void hh_walk_mask(const hh_ctx *c, const hh_masks *mk, uint32_t lane, uint32_t S,
-                        uint32_t x, hh_rec *r) {
-    r->k = 1; r->e = 0; r->delta = 0; r->cov = 0;
-    uint32_t A = x;
-    uint32_t R = lane + 1;
-    if (A < R * S) return;      /* stream ended inside this region */
-    for (uint32_t it = 0; it < HH_KM; it++, R++) {
-        const uint32_t Lr = R * S, Le = Lr + S;
-        const uint32_t eA = A - Lr;
-        uint32_t ca = 0;
-        if (R < mk->nreg) {
-            const uint32_t *m = mk->m + R * mk->mw;
-            const uint32_t lim = Le < c->bt ? Le : c->bt;
-            while (A < lim) {
-                uint32_t win = hh_read32(c, A);
-                uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-                uint32_t ns = HH_L1_NSYM(e), l, bm = 1u;
-                if (ns && A + HH_L1_NBITS(e) <= lim) {
-                    l = HH_L1_NBITS(e);
-                    bm = HH_L1_BMASK(e);
-                } else {
-                    if (ns) {
-                        l = HH_L1_LEN0(e);
-                    } else {
-                        uint32_t s;
-                        l = hh_escape(c, A, win, e, &s);
-                    }
-                    ns = 1;
-                }
-                const uint32_t off = A - Lr, wi = off >> 5, sh = off & 31u;
-                uint64_t mm = (uint64_t)m[wi];
-                if (wi + 1 < mk->mw) mm |= (uint64_t)m[wi + 1] << 32;
-                const uint32_t hit = bm & (uint32_t)(mm >> sh);
-                if (hit) {
-                    const uint32_t t = (uint32_t)__builtin_ctz(hit);
-                    const uint32_t a = ca + (uint32_t)__builtin_popcount(bm & ((1u << t) - 1u));
-                    const uint32_t b = hh_mask_rank(mk, R, off + t);
-                    r->k = it + 1;
-                    r->e = eA;
-                    r->delta = (int32_t)a - (int32_t)b;
-                    return;
-                }
-                uint32_t rem = c->bt - A;
-                A += l < rem ? l : rem;
-                ca += ns;
-            }
-            /* both chains leave the region at the same point -> merged there */
-            if (A == Lr + mk->x[R] || A >= c->bt) {
-                r->k = it + 1;
-                r->e = eA;
-                r->delta = (int32_t)ca - (int32_t)mk->n[R];
-                return;
-            }
-        } else {
-            uint32_t B = Lr, cb = 0;
-            for (;;) {
-                if (A == B) {
-                    r->k = it + 1;
-                    r->e = eA;
-                    r->delta = (int32_t)ca - (int32_t)cb;
-                    return;
-                }
-                uint32_t ad = A >= Le, bd = B >= Le;
-                if (ad && bd) break;
-                if (!ad && (bd || A < B)) {
-                    A += hh_len1(c, A);
-                    ca++;
-                } else {
-                    B += hh_len1(c, B);
-                    cb++;
-                }
-            }
-        }
-        r->cov += ca;
+/* Live masks: bit d of mem[j] <=> lane j is live for entering d.  The
+ * exceptions (k > 1), in ascending lane order, clear the lanes they cover
+ * for the entering states that reach them. */
+HH_HD uint32_t hh_mem_init(uint32_t j) { return j < HH_KM - 1 ? (2u << j) - 1u : (1u << HH_KM) - 1u; }
+
+/* Pass 3 (calcresult restated), one step of a lane's emission: the run is
+ * [p, pe) on the true chain (pe a boundary of it, or bt), the output window
+ * ends at whi.  Takes a whole lookup when it fits both, else one symbol
+ * (with the tail rule at bt).  Returns the symbols taken (k) in *val (first
+ * in bits 0..7) and the bits advanced. */
+HH_HD uint32_t hh_emit_step(const hh_ctx *c, uint32_t p, uint32_t pe, uint64_t o, uint64_t whi,
+                            uint32_t *val, uint32_t *k) {
+    hh_look L = hh_lookup(c, p);
+    if (p + L.nb <= pe && o + L.ns <= whi) {
+        *val = L.syms;
+        *k = L.ns;
+        return L.nb;
     }
-    r->k = 0;
+    uint32_t adv = L.len0, s = L.syms & 0xffu;
+    if (adv > c->bt - p) {
+        s = hh_tail_symbol(c, p);
+        adv = c->bt - p;
+    }
+    *val = s;
+    *k = 1;
+    return adv;
 }
 
 /* ------------------------------------------------------------------ */
-/* Cross-tile state and tile transfer tables.                          */
-/* The state entering a tile: d = first live lane of the tile (lanes    */
-/* before it are covered by a walk from the previous tile), e = its     */
-/* entry offset, delta = its count correction.  A tile table maps every */
-/* d in [0, HH_KM) to the state leaving the tile and the number of      */
-/* symbols the tile's live lanes emit (delta of the entering lane not   */
-/* included -- it is added when tables are applied).                   */
+/* Cross-tile granules (64-bit, status in bits 62..63, 0 = not yet).   */
+/*   aggregate (status 1): the table entry for d = 0, bit 61 CONST: the  */
+/*     leaving state is the same for every entering d.                   */
+/*   inclusive (status 2): bits 0..39 charged prefix through the tile,   */
+/*     bits 40..60 the tile's resolved leaving state.                    */
 /* ------------------------------------------------------------------ */
-HH_HD uint64_t hh_xf_pack(uint32_t count, int32_t delta, uint32_t e, uint32_t d) {
-    return (uint64_t)count | ((uint64_t)((uint32_t)delta & 0xffffu) << 32) |
-           ((uint64_t)(e & 0xfffu) << 48) | ((uint64_t)(d & 0xfu) << 60);
+#define HH_ST_SHIFT 62
+#define HH_AGG (1ull << 62)
+#define HH_INC (2ull << 62)
+#define HH_CST (1ull << 61)
+#define HH_INC_MASK ((1ull << 40) - 1ull)
+
+HH_HD uint64_t hh_inc_pack(uint64_t prefix, uint32_t state) {
+    return HH_INC | (prefix & HH_INC_MASK) | ((uint64_t)state << 40);
 }
-HH_HD uint32_t hh_xf_count(uint64_t v) { return (uint32_t)v; }
-HH_HD int32_t hh_xf_delta(uint64_t v) { return (int32_t)(int16_t)(uint16_t)(v >> 32); }
-HH_HD uint32_t hh_xf_e(uint64_t v) { return (uint32_t)(v >> 48) & 0xfffu; }
-HH_HD uint32_t hh_xf_d(uint64_t v) { return (uint32_t)(v >> 60); }
+HH_HD uint32_t hh_inc_state(uint64_t g) { return (uint32_t)(g >> 40) & 0x1fffffu; }
 
-/* Tile state: packed (d, e, delta) + 64-bit output base. */
-typedef struct {
-    uint32_t d, e;
-    int32_t delta;
-    uint64_t base;
-} hh_state;
-
-/* Apply a tile table to the entering state. */
-HH_HD hh_state hh_xf_apply(const uint64_t *tab, hh_state s) {
-    uint64_t v = tab[s.d];
-    hh_state o;
-    o.base = s.base + (uint64_t)((int64_t)hh_xf_count(v) + s.delta);
-    o.d = hh_xf_d(v);
-    o.e = hh_xf_e(v);
-    o.delta = hh_xf_delta(v);
-    return o;
-}
-
-/* Generic composed function over d (64-bit counts): used by the scan. */
-typedef struct {
-    uint8_t d[HH_KM];
-    uint16_t e[HH_KM];
-    int16_t delta[HH_KM];
-    uint64_t cnt[HH_KM];
-} hh_fn;
-
-HH_HD void hh_fn_from_tab(const uint64_t *tab, hh_fn *f) {
-    for (int i = 0; i < HH_KM; i++) {
-        uint64_t v = tab[i];
-        f->d[i] = (uint8_t)hh_xf_d(v);
-        f->e[i] = (uint16_t)hh_xf_e(v);
-        f->delta[i] = (int16_t)hh_xf_delta(v);
-        f->cnt[i] = hh_xf_count(v);
-    }
-}
-
-/* h = g after f (f applied first). */
-HH_HD void hh_fn_compose(const hh_fn *f, const hh_fn *g, hh_fn *h) {
-    hh_fn t;
-    for (int i = 0; i < HH_KM; i++) {
-        uint32_t j = f->d[i];
-        uint8_t gd = 0; uint16_t ge = 0; int16_t gdel = 0; uint64_t gc = 0;
-        for (int m = 0; m < HH_KM; m++) {   /* select, no dynamic indexing */
-            if ((uint32_t)m == j) { gd = g->d[m]; ge = g->e[m]; gdel = g->delta[m]; gc = g->cnt[m]; }
-        }
-        t.d[i] = gd; t.e[i] = ge; t.delta[i] = gdel;
-        t.cnt[i] = (uint64_t)((int64_t)f->cnt[i] + f->delta[i]) + gc;
-    }
-    *h = t;
-}
-
-HH_HD hh_state hh_fn_apply(const hh_fn *f, hh_state s) {
-    hh_state o = s;
-    for (int m = 0; m < HH_KM; m++) {
-        if ((uint32_t)m == s.d) {
-            o.base = s.base + (uint64_t)((int64_t)f->cnt[m] + s.delta);
-            o.d = f->d[m]; o.e = f->e[m]; o.delta = f->delta[m];
-        }
-    }
-    return o;
-}
-
-/* ------------------------------------------------------------------ */
-/* Sequential reference forms of the tile resolution (the kernels do   */
-/* the same with ballots and LDS; the emulator and the host use these). */
-/* ------------------------------------------------------------------ */
-HH_HD uint32_t hh_rec_next(uint32_t j, const hh_rec &r) { return j + (r.k ? r.k : 1u); }
-
-/* Tile table over nr regions: for each entering d, follow j -> j + k_j. */
-HH_HD void hh_tile_table_seq(const uint64_t *rec, uint32_t nr, uint64_t *tab) {
-    for (uint32_t d = 0; d < HH_KM; d++) {
-        uint32_t j = d, cnt = 0;
-        for (;;) {
-            hh_rec r = hh_rec_unpack(rec[j]);
-            uint32_t nx = hh_rec_next(j, r);
-            cnt += r.n + r.cov;
-            if (nx >= nr) { tab[d] = hh_xf_pack(cnt, r.delta, r.e, nx - nr); break; }
-            cnt = (uint32_t)((int32_t)cnt + r.delta);
-            j = nx;
-        }
-    }
-}
-
-/* Emit one run: decode from *pp while p < pe (a code boundary or bt) and
- * the output index stays below wend.  sink(o, byte) stores a symbol. */
-template <class Sink>
-HH_HD void hh_emit_run(const hh_ctx *c, uint32_t *pp, uint32_t pe, uint64_t *po,
-                       uint64_t wend, Sink &sink) {
-    uint32_t p = *pp;
-    uint64_t o = *po;
-    while (p < pe && o < wend) {
-        uint32_t win = hh_read32(c, p);
-        uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-        uint32_t ns = HH_L1_NSYM(e);
-        if (ns && p + HH_L1_NBITS(e) <= pe && o + ns <= wend) {
-            uint32_t syms = HH_L1_SYMS(e);
-            sink(o, syms & 0xffu);
-            if (ns > 1) sink(o + 1, (syms >> 8) & 0xffu);
-            if (ns > 2) sink(o + 2, (syms >> 16) & 0xffu);
-            if (ns > 3) sink(o + 3, syms >> 24);
-            p += HH_L1_NBITS(e);
-            o += ns;
-        } else {
-            uint32_t s;
-            uint32_t l = hh_dec1(c, p, &s);
-            sink(o, s);
-            p += l;
-            o++;
-        }
-    }
-    *pp = p;
-    *po = o;
+/* Region size for a code whose lengths are all multiples of g: a multiple
+ * of 32 (whole words per region column) and of g (region starts on the
+ * code lattice, or chains of fixed-length codes could never meet), near
+ * 256 bits.  0 if none fits HH_SW_MAX words. */
+HH_HD uint32_t hh_pick_region_bits(uint32_t g) {
+    if (g == 0) g = 1;
+    uint32_t a = 32, b = g;
+    while (b) { uint32_t t = a % b; a = b; b = t; }
+    uint32_t l = 32 / a * g;          /* lcm(32, g) */
+    if (l > 32 * HH_SW_MAX) return 0;
+    uint32_t S = l;
+    while (S + l <= 256) S += l;
+    if (S < 128 && S + l <= 32 * HH_SW_MAX) S += l;
+    return S;
 }
 
 #endif

@@ -1,13 +1,24 @@
 // hh_device.hip -- HIP kernels (gfx950) and the device half of the C ABI.
 //
 // Fast path: ONE persistent launch, k_decode (O(N) memory, 64-bit offsets).
-// Tiles of HH_NR regions of S bits are dispensed in order; each workgroup
-// keeps two in flight: while it decodes tile B's regions from offset 0 with
-// boundary masks (decodeallbits) it emits tile A's runs (calcresult), then
-// walks B's region exits into their successors until the chains share a
-// boundary (makebigtable) and publishes B's transfer table.  Output bases
-// come from a decoupled look-back over those tables (calcbitsindex /
-// findmax).  C is read once from HBM, D written once.
+// Workgroup b takes tiles b, b + G, b + 2G, ... (G = resident grid).  Per
+// tile of HH_NR regions x S bits:
+//   stage     the tile's words (+ next tile's first region + a halo), loaded
+//             by each lane for its own region column one tile ahead, stored
+//             to LDS transposed (conflict-free per-lane reads)
+//   pass 1    every lane decodes its region from offset 0: count, exit
+//             (decodeallbits)
+//   walks     each exit is walked against the next region's chain until the
+//             two share a boundary: delta (makebigtable)
+//   publish   the tile's charged count sum(n + delta) -- independent of the
+//             tile's entry -- with its last exit/delta (aggregate granule)
+//   pass 2    lanes re-decode their exact runs into an LDS output window,
+//             dword writes (calcresult); windows larger than the buffer go
+//             in rounds
+//   look-back decoupled look-back over the aggregates -> output base
+//             (calcbitsindex / findmax), inclusive granule published
+//   copy      LDS window -> HBM with 16-byte aligned coalesced stores
+// C is read from HBM once and D written once.
 // Reference-shaped stage kernels (k_st_*) mirror the six .cl kernels one by
 // one for intermediate-array parity.
 #include <hip/hip_runtime.h>
@@ -21,11 +32,8 @@
 #include "hh_internal.h"
 #include "hiphuff.h"
 
-#define HH_S_DEFAULT 288          // 9 words: odd word stride spreads LDS banks
-#define HH_S_MAX 320
-#define HH_SPAN_MARGIN 320        // bits beyond the last walk region
-#define HH_NW_MAX (((HH_NL + HH_KM + 1) * HH_S_MAX + HH_SPAN_MARGIN) / 32 + 4)
-#define HH_MAXLEN_FAST 256        // longest code the fast path stages for
+#define HH_OB_DEFAULT (32u << 10)   // LDS output window per workgroup (bytes)
+#define HH_MAXLEN_FAST 64           // longest code the fast path stages for
 
 #define HIP_OK(x)                                                             \
     do {                                                                      \
@@ -36,6 +44,8 @@
         }                                                                     \
     } while (0)
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 struct DevTab {
     const uint64_t *l1;
     const uint32_t *l2;
@@ -44,83 +54,16 @@ struct DevTab {
     uint32_t l2_used;
 };
 
-// flags[0]: bit0 walk failed, bit1 output overflow, bit2 count mismatch
-// flags[2..3]: total symbols (u64, written by k_scan)
-enum { F_FAIL = 1, F_OVER = 2, F_MISMATCH = 4 };
+// flags[0]: status bits; flags[2..3]: total symbols (u64, last tile)
+enum { F_FAIL = 1, F_OVER = 2, F_TIMEOUT = 8 };
+#define HH_SPIN_LIMIT (1u << 22)
 
-// ---------------------------------------------------------------------------
-// shared helpers
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// Exclusive block scan of u32 (blockDim == HH_NL, 4 waves).
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_tmp, uint32_t *total) {
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) s_tmp[wv] = x;
-    __syncthreads();
-    uint32_t base = 0, tot = 0;
-    for (uint32_t i = 0; i < HH_NL / 64; i++) {
-        uint32_t t = s_tmp[i];
-        if (i < wv) base += t;
-        tot += t;
-    }
-    *total = tot;
-    __syncthreads();
-    return base + x - v;
-}
-
-// The exceptions (walks with k > 1) of a tile, ascending, into s_exc.
-__device__ __forceinline__ uint32_t collect_exceptions(bool is_exc, uint16_t *s_exc, uint32_t *s_cnt4) {
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint64_t m = __ballot(is_exc);
-    if (lane == 0) s_cnt4[wv] = __popcll(m);
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-    for (uint32_t i = 0; i < HH_NL / 64; i++) {
-        if (i < wv) off += s_cnt4[i];
-        tot += s_cnt4[i];
-    }
-    if (is_exc) {
-        uint64_t below = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
-        s_exc[off + __popcll(below)] = (uint16_t)threadIdx.x;
-    }
-    __syncthreads();
-    return tot;
-}
-
-// ---------------------------------------------------------------------------
-// The fused decoder: one persistent kernel, tiles dispensed in order.
-//
-// Per tile: (1) stage the tile's bits (+ halo) in LDS; (2) every lane
-// decodes its region from offset 0 and walks its exit into the next region
-// until the chains share a boundary; (3) the tile resolves its live lanes for
-// every entering state d and publishes its HH_KM-entry transfer table
-// (AGGREGATE); (4) decoupled look-back over predecessors' tables / inclusive
-// states yields this tile's entering state and output base, published as
-// INCLUSIVE; (5) live lanes re-decode their runs into an LDS window, written
-// out with 16-byte stores.  C is read once, D written once.
-// ---------------------------------------------------------------------------
 struct LookBack {
-    uint64_t *gran;      // [ntiles] tagged granule: table published (+ count, state for d = 0)
-    uint64_t *incl;      // [ntiles] tagged inclusive prefix of charged counts
-    uint64_t *xst;       // [ntiles] tagged resolved outgoing state
-    uint64_t *tabs;      // [ntiles][HH_KM] tile tables (sc1 stores)
-    uint32_t *counter;   // tile dispenser
+    uint64_t *agg;       // [ntiles] aggregate granules (table entry d = 0 + CONST)
+    uint64_t *inc;       // [ntiles] inclusive granules (prefix + resolved state)
+    uint64_t *tdbg;      // diagnostic (HH_DEBUG_TILES): [ntiles][8] base, size|state, excl, table entry,
+                         //   look-back: inclusive tile, its prefix, counts summed, rounds
 };
-
-// 64-bit granules: the data is the flag (bits 62..63 = status, 0 = not yet).
-#define HH_ST_SHIFT 62
-#define HH_VAL_MASK ((1ull << HH_ST_SHIFT) - 1ull)
 
 __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -129,51 +72,49 @@ __device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-enum { F_TIMEOUT = 8 };
-
 // Diagnostic build only (-DHH_STAMPS): wave 0 of every workgroup adds the
 // shader-clock cycles of each phase into dbg[block][phase].
 #define HH_NDBG 12
 #ifdef HH_STAMPS
-#define HH_NSTAMP HH_NDBG
-#define STAMP_DECL uint64_t st_acc[HH_NSTAMP] = {0}; uint64_t st_t = __builtin_amdgcn_s_memtime();
+#define STAMP_DECL uint64_t st_acc[HH_NDBG] = {0}; uint64_t st_t = __builtin_amdgcn_s_memtime();
 #define STAMP(i) do { uint64_t t_ = __builtin_amdgcn_s_memtime(); st_acc[i] += t_ - st_t; st_t = t_; } while (0)
-#define STAMP_FLUSH(dbg) do { if (threadIdx.x == 0) for (int i_ = 0; i_ < HH_NSTAMP; i_++) (dbg)[blockIdx.x * HH_NSTAMP + i_] = st_acc[i_]; } while (0)
+#define STAMP_FLUSH(dbg) do { if (threadIdx.x == 0) for (int i_ = 0; i_ < HH_NDBG; i_++) (dbg)[blockIdx.x * HH_NDBG + i_] = st_acc[i_]; } while (0)
 #define COUNT(i, v) do { st_acc[i] += (v); } while (0)
-#define HH_TDBG_MAX (1u << 18)
-#define TSTAMP(t, k) do { if (threadIdx.x == 0 && (t) < HH_TDBG_MAX) dbg[gridDim.x * HH_NDBG + (t) * 6 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
-#define COUNT(i, v) do {} while (0)
-#define TSTAMP(t, k) do {} while (0)
 #define STAMP_DECL
 #define STAMP(i) do {} while (0)
 #define STAMP_FLUSH(dbg) do {} while (0)
+#define COUNT(i, v) do {} while (0)
 #endif
-#define HH_SPIN_LIMIT (1u << 22)
 
-// Stage n u64 / u32 table words with all loads issued before any LDS store.
-template <uint32_t N>
-__device__ __forceinline__ void stage_l1(uint64_t *dst, const uint64_t *src) {
-    constexpr uint32_t PER = N / HH_NL;
-    uint64_t v[PER];
+// Inclusive wave scan (64 lanes) of u32.
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t x) {
+    const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
-    for (uint32_t k = 0; k < PER; k++) v[k] = src[threadIdx.x + k * HH_NL];
-#pragma unroll
-    for (uint32_t k = 0; k < PER; k++) dst[threadIdx.x + k * HH_NL] = v[k];
+    for (int o = 1; o < 64; o <<= 1) {
+        int32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    return x;
 }
 
-// Poll a tagged granule until its status bits are non-zero (bounded).
-__device__ __forceinline__ uint64_t poll_granule(const uint64_t *p, uint32_t *flags) {
-    uint64_t v;
-    uint32_t spins = 0;
-    while (((v = ld_sc1(p)) >> HH_ST_SHIFT) == 0) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > HH_SPIN_LIMIT) {
-            atomicOr(flags, (uint32_t)F_TIMEOUT);
-            return 3ull << HH_ST_SHIFT;
-        }
+// Exclusive block scan of int32 over HH_NL lanes; *total = block sum.
+__device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t *s_tmp, int32_t *total) {
+    constexpr uint32_t NW = HH_NL / 64;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const int32_t x = wave_incl_scan(v);
+    if (lane == 63) s_tmp[wv] = x;
+    __syncthreads();
+    int32_t base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < NW; i++) {
+        const int32_t t = s_tmp[i];
+        base += i < wv ? t : 0;
+        tot += t;
     }
-    return v;
+    *total = tot;
+    __syncthreads();
+    return base + x - v;
 }
 
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
@@ -185,461 +126,437 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
     return v;
 }
 
-// Regions per tile: the last lane decodes the NEXT tile's first region too
-// (its mask lets the tile's last walk merge without a two-pointer walk).
-#define HH_NR (HH_NL - 1)
-
-// Granule layout (gran[t], status 1 = tile t's table is published):
-//   bits  0..19 count_t(0), signed: symbols charged to the tile for d = 0
-//   bits 20..23 d_out, 24..35 e_out, 36..51 delta_out (the state for d = 0)
-//   bit  61     CONST: every entering d leads to that same outgoing state
-// Charging: count_t(d) = sum over the tile's live lanes of n + cov + delta,
-// i.e. each walk's correction is charged to the walker's tile, so a tile's
-// count depends on its predecessor only through d.  The first run of tile t
-// then starts delta_in(t) symbols before the charged prefix of tiles < t.
-#define HH_GR_PUB (1ull << 62)
-#define HH_GR_CST (1ull << 61)
-#define HH_INCL (2ull << 62)
-
-__device__ __forceinline__ uint64_t gran_pack(uint64_t xf, bool cst) {
-    return HH_GR_PUB | (cst ? HH_GR_CST : 0ull) | (uint64_t)(hh_xf_count(xf) & 0xfffffu) |
-           ((uint64_t)hh_xf_d(xf) << 20) | ((uint64_t)hh_xf_e(xf) << 24) |
-           ((uint64_t)((uint32_t)hh_xf_delta(xf) & 0xffffu) << 36);
-}
-__device__ __forceinline__ int32_t gran_cnt(uint64_t g) { return ((int32_t)((uint32_t)g << 12)) >> 12; }
-// entering-state word of the successor: d | e << 4 | delta << 16
-__device__ __forceinline__ uint64_t gran_state(uint64_t g) {
-    return ((g >> 20) & 0xfu) | (((g >> 24) & 0xfffu) << 4) | (((g >> 36) & 0xffffu) << 16);
-}
-__device__ __forceinline__ uint64_t xf_state(uint64_t xf) {
-    return (uint64_t)hh_xf_d(xf) | ((uint64_t)hh_xf_e(xf) << 4) |
-           ((uint64_t)((uint32_t)hh_xf_delta(xf) & 0xffffu) << 16);
+// Poll a granule until its status bits are non-zero (bounded).
+__device__ __forceinline__ uint64_t poll_granule(const uint64_t *p, uint32_t *flags) {
+    uint64_t v;
+    uint32_t spins = 0;
+    while (((v = ld_sc1(p)) >> HH_ST_SHIFT) == 0) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > HH_SPIN_LIMIT) {
+            atomicOr(flags, (uint32_t)F_TIMEOUT);
+            return HH_AGG;   // zero count: the decode is reported as failed
+        }
+    }
+    return v;
 }
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
-    const uint32_t lo = __shfl((uint32_t)v, (int)src, 64), hi = __shfl((uint32_t)(v >> 32), (int)src, 64);
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = __shfl((uint32_t)v, src, 64), hi = __shfl((uint32_t)(v >> 32), src, 64);
     return ((uint64_t)hi << 32) | lo;
 }
 
-// Charged symbols of tiles < A (A >= 1), one wave.  64 predecessors per
-// round: granule, inclusive word and the granule before it (which gives the
-// predecessor's entering d).  The nearest inclusive prefix ends the round;
-// the window's own inclusive prefixes are then published too, so later
-// look-backs stop early.  Returns false if an entering d in the window is
-// not CONST-resolvable (rare: caller takes the serial path).
-#ifdef HH_STAMPS
-#define COUNT_LB(i, v) do { lbd[i] += (v); } while (0)
-#else
-#define COUNT_LB(i, v) do {} while (0)
-#endif
-__device__ bool lookback_excl(const LookBack &lb, uint64_t A, uint32_t *flags, uint64_t *excl_out,
-                              uint32_t *nrounds, uint32_t *nspins, uint64_t *lbd) {
+// State entering tile t: the leaving state of tile t-1, read from its
+// aggregate when that is CONST (the common case: available as soon as t-1's
+// walks are done), else from its inclusive granule (t-1 resolved its own
+// entering state first).
+__device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t *flags) {
+    if (t == 0) return hh_state_pack(0, 0, 0);
+    const uint64_t g = poll_granule(&lb.agg[t - 1], flags);
+    if (g & HH_CST) return hh_tab_state(g);
+    return hh_inc_state(poll_granule(&lb.inc[t - 1], flags));
+}
+
+// Exclusive charged prefix of tile t (t >= 1), one wave: 64 predecessors per
+// round, the nearest inclusive granule ends the look-back.  A tile's
+// aggregate is its count for entering d = 0; the state entering tile u comes
+// from the inclusive of u-1 if that is the nearest one, else from u-1's
+// aggregate, which must be CONST.  Otherwise (or if u is entered with d > 0)
+// the look-back waits until an inclusive granule appears closer.
+#define HH_LBV 8   // tiles per lane per look-back round (512-tile window)
+__device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flags) {
+    constexpr uint32_t V = HH_LBV;
     const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t st0 = HH_AGG | HH_CST | hh_tab_pack(0, hh_state_pack(0, 0, 0));
+    const uint64_t in0 = hh_inc_pack(0, hh_state_pack(0, 0, 0));
     uint64_t excl = 0;
-    int64_t top = (int64_t)A - 1;
-    int32_t c0 = 0;
-    uint32_t first0 = 64;
-    bool r0 = true;
+    int64_t top = (int64_t)t - 1;
+    uint32_t rounds = 0;
     for (;;) {
-        const int64_t idx = top - (int64_t)lane;
-        uint64_t iv = HH_INCL, gv = HH_GR_PUB | HH_GR_CST, gp = HH_GR_PUB | HH_GR_CST;
-        uint32_t first, spins = 0;
+        // this lane: tiles ub, ub-1, ..., ub-V+1 (window offsets lane*V + i)
+        const int64_t ub = top - (int64_t)(lane * V);
+        uint64_t iv[V], av[V + 1];
+        uint32_t ofirst, spins = 0, lf;
+        uint64_t incv;
         for (;;) {
-            if (idx >= 0) {
-                iv = ld_sc1(&lb.incl[idx]);
-                gv = ld_sc1(&lb.gran[idx]);
+#pragma unroll
+            for (uint32_t i = 0; i <= V; i++) {
+                const int64_t u = ub - (int64_t)i;
+                if (i < V) iv[i] = u >= 0 ? ld_sc1(&lb.inc[u]) : in0;
+                av[i] = u >= 0 ? ld_sc1(&lb.agg[u]) : st0;
             }
-            if (idx >= 1) gp = ld_sc1(&lb.gran[idx - 1]);
-            const uint64_t inc = __ballot((iv >> HH_ST_SHIFT) == 2);
-            first = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;
-            const uint64_t miss = __ballot(lane < first && ((gv >> HH_ST_SHIFT) == 0 || (gp >> HH_ST_SHIFT) == 0));
-            if (!miss) break;
-            COUNT_LB(0, __builtin_ctzll(miss));
-            COUNT_LB(1, 63 - __builtin_clzll(miss));
-            COUNT_LB(2, (__ballot(lane < first && (gv >> HH_ST_SHIFT) == 0) != 0));
-            COUNT_LB(3, first);
+            lf = V;
+#pragma unroll
+            for (int i = (int)V - 1; i >= 0; i--)
+                if ((iv[i] >> HH_ST_SHIFT) == 2) lf = (uint32_t)i;
+            const uint64_t m = __ballot(lf < V);
+            const uint32_t fl = m ? (uint32_t)__builtin_ctzll(m) : 64u;
+            const uint32_t lff = (uint32_t)__shfl((int)lf, (int)(fl & 63u), 64);
+            ofirst = fl < 64 ? fl * V + lff : 64u * V;
+            // the nearest inclusive granule (value and resolved state)
+            uint64_t myinc = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < V; i++) if (i == lf) myinc = iv[i];
+            incv = shfl64(myinc, (int)(fl & 63u));
+            bool ok = true;
+#pragma unroll
+            for (uint32_t i = 0; i < V; i++) {
+                const uint32_t o = lane * V + i;
+                if (o < ofirst) {
+                    const bool pin = o + 1 == ofirst;
+                    const uint64_t pv = av[i + 1];
+                    const bool known = pin || ((pv >> HH_ST_SHIFT) != 0 && (pv & HH_CST));
+                    const uint32_t st = pin ? hh_inc_state(incv) : hh_tab_state(pv);
+                    // entered with d > 0: row d = 0 does not apply, wait for the
+                    // tile's own inclusive prefix
+                    ok = ok && (av[i] >> HH_ST_SHIFT) != 0 && known && hh_state_d(st) == 0;
+                }
+            }
+            if (!__ballot(!ok)) break;
             __builtin_amdgcn_s_sleep(1);
             if (++spins > HH_SPIN_LIMIT) {
                 if (lane == 0) atomicOr(flags, (uint32_t)F_TIMEOUT);
-                *excl_out = 0;
-                return true;
+                return 0;
             }
         }
-        *nrounds += 1;
-        *nspins += spins;
-        if (__ballot(lane < first && !(gp & HH_GR_CST))) return false;
-        int32_t c = 0;
-        if (lane < first) {
-            const uint32_t din = (uint32_t)(gp >> 20) & 0xfu;
-            c = din == 0 ? gran_cnt(gv) : (int32_t)hh_xf_count(ld_sc1(&lb.tabs[idx * HH_KM + din]));
-        }
-        excl += wave_sum64((uint64_t)(int64_t)c);
-        if (first < 64) excl += shfl64(iv, first) & HH_VAL_MASK;
-        if (r0) {
-            c0 = c;
-            first0 = first;
-            r0 = false;
-        }
-        if (first < 64) break;
-        top -= 64;
-    }
-    // inclusive prefixes of the first window: incl[A-1-i] = excl - sum_{j<i} c0_j
-    int32_t x = c0;
+        int64_t c = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
+        for (uint32_t i = 0; i < V; i++)
+            if (lane * V + i < ofirst) c += hh_tab_count(av[i]);
+        excl += wave_sum64((uint64_t)c);
+        rounds++;
+        if (ofirst < 64u * V) {
+            const uint64_t pre = incv & HH_INC_MASK;
+            if (lb.tdbg && lane == 0) {
+                lb.tdbg[t * 8 + 4] = (uint64_t)(top - (int64_t)ofirst);
+                lb.tdbg[t * 8 + 5] = pre;
+                lb.tdbg[t * 8 + 6] = excl;
+                lb.tdbg[t * 8 + 7] = rounds;
+            }
+            return excl + pre;
+        }
+        top -= (int64_t)(64u * V);
     }
-    if (lane < first0) st_sc1(&lb.incl[A - 1 - lane], ((excl - (uint64_t)(int64_t)(x - c0)) & HH_VAL_MASK) | HH_INCL);
-    *excl_out = excl;
-    return true;
 }
 
-// Tile staging: a tile's words (+ halo) are loaded to registers, then stored
-// to LDS.  Plain loads: the emission pass re-stages the same words two
-// iterations later, from L2.
-#define HH_STAGE_PER ((HH_NW_MAX + HH_NL - 1) / HH_NL)
-struct Staged {
-    uint32_t v[HH_STAGE_PER];
+// Stream word gi, zero past the readable payload.
+__device__ __forceinline__ uint32_t ld_word(const uint32_t *g, uint64_t gi, uint64_t nok) {
+    return gi < nok ? __builtin_nontemporal_load(&g[gi]) : 0u;
+}
+
+// Registers holding one tile's words for this lane: its region column and,
+// for lanes < (HH_NCOL - HH_NR) * sw, one word of the columns past the tile
+// (the next tile's first HH_KM regions and the halo).
+#define HH_XW ((HH_NCOL - HH_NR) * HH_SW_MAX)
+static_assert(HH_XW <= HH_NL, "extra columns must fit one word per lane");
+struct Prefetch {
+    uint32_t v[HH_SW_MAX];
+    uint32_t halo;
 };
-__device__ __forceinline__ void stage_load(Staged &s, const uint32_t *g, uint64_t w0, uint32_t nw,
-                                           uint64_t nwords_ok) {
+
+template <uint32_t sw>
+__device__ __forceinline__ void prefetch_tile(Prefetch &pf, const uint32_t *g, uint64_t tw0,
+                                              uint64_t nok, bool vec4) {
+    const uint32_t j = threadIdx.x;
+    const uint64_t gi = tw0 + (uint64_t)j * sw;
+    if (sw % 4 == 0 && vec4 && gi + HH_SW_MAX <= nok) {
 #pragma unroll
-    for (uint32_t k = 0; k < HH_STAGE_PER; k++) {
-        const uint32_t i = threadIdx.x + k * HH_NL;
-        const uint64_t gi = w0 + i;
-        s.v[k] = (i < nw && gi < nwords_ok) ? g[gi] : 0u;
+        for (uint32_t k = 0; k < HH_SW_MAX; k += 4) {
+            if (k < sw) {
+                const u32x4 q = __builtin_nontemporal_load((const u32x4 *)(g + gi + k));
+                pf.v[k] = q.x; pf.v[k + 1] = q.y; pf.v[k + 2] = q.z; pf.v[k + 3] = q.w;
+            }
+        }
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < HH_SW_MAX; k++)
+            if (k < sw) pf.v[k] = ld_word(g, gi + k, nok);
     }
+    pf.halo = j < (HH_NCOL - HH_NR) * sw ? ld_word(g, tw0 + (uint64_t)HH_NR * sw + j, nok) : 0u;
 }
-__device__ __forceinline__ void stage_store(const Staged &s, uint32_t *dst, uint32_t nw) {
+
+template <uint32_t sw>
+__device__ __forceinline__ void store_tile(const Prefetch &pf, uint32_t *s_w) {
+    const uint32_t j = threadIdx.x;
 #pragma unroll
-    for (uint32_t k = 0; k < HH_STAGE_PER; k++) {
-        const uint32_t i = threadIdx.x + k * HH_NL;
-        if (i < nw) dst[i] = s.v[k];
+    for (uint32_t k = 0; k < HH_SW_MAX; k++)
+        if (k < sw) s_w[k * HH_NLS + j] = pf.v[k];
+    if (j < (HH_NCOL - HH_NR) * sw) s_w[(j % sw) * HH_NLS + HH_NR + j / sw] = pf.halo;
+}
+
+// The walks with k > 1 (exceptions) of a tile, ascending, into s_exc.
+__device__ __forceinline__ uint32_t collect_exceptions(bool is_exc, uint16_t *s_exc, uint32_t *s_cnt) {
+    constexpr uint32_t NW = HH_NL / 64;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const uint64_t m = __ballot(is_exc);
+    if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t off = 0, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < NW; i++) {
+        off += i < wv ? s_cnt[i] : 0u;
+        tot += s_cnt[i];
     }
+    if (is_exc) {
+        const uint64_t below = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
+        s_exc[off + (uint32_t)__popcll(below)] = (uint16_t)threadIdx.x;
+    }
+    __syncthreads();
+    return tot;
+}
+
+__device__ __forceinline__ int32_t wave_sum(int32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
 // ---------------------------------------------------------------------------
-// k_decode: persistent; a workgroup holds three tiles.  Iteration i:
-//   (1) take tile B (dispenser) and load its bits (+ halo) into registers;
-//       re-stage the bits of tile A (taken in iteration i-2) from L2;
-//   (2) tile A: output base by look-back over its predecessors' granules.
-//       Those were published when their tiles were decoded, at least one
-//       full iteration ago, and a granule is published before its
-//       workgroup's own look-back -- so a look-back never waits on a tile
-//       whose publication itself waits (emitting one iteration after the
-//       decode instead lets waits feed on waits without bound);
-//       then A's live lanes and run offsets;
-//   (3) one loop, two independent chains per lane: B's offset-0 region
-//       decode with its boundary mask (decodeallbits) and A's run emission
-//       (calcresult), dword stores straight to HBM;
-//   (4) B's walks (makebigtable) and transfer table, published with its
-//       granule.  Then A <- P (the tile decoded in iteration i-1), P <- B.
-// C is read from HBM once (the re-stage hits L2) and D written once.
+// k_decode
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(HH_NL) void k_decode(const uint32_t *__restrict__ gdata, uint64_t bits,
-                                                  uint64_t nwords_ok, uint32_t S, DevTab tab,
-                                                  uint64_t ntiles, LookBack lb,
+struct Geometry {
+    uint64_t bits;       // stream length
+    uint64_t nwords;     // readable payload words
+    uint64_t ntiles;
+    uint32_t S, sw, magic;
+    uint32_t ob;         // LDS output window bytes (multiple of 16)
+    uint32_t vec4;       // 16-B aligned payload and sw % 4 == 0
+};
+
+template <uint32_t SW>
+__global__ __launch_bounds__(HH_NL, 4) void k_decode(const uint32_t *__restrict__ gdata, Geometry geo,
+                                                  DevTab tab, LookBack lb,
                                                   uint8_t *__restrict__ out, uint64_t cap,
                                                   uint32_t *flags, uint64_t *dbg) {
-    __shared__ uint64_t s_l1[HH_L1_SIZE];
-    __shared__ uint32_t s_w[2 * HH_NW_MAX];
-    __shared__ uint32_t s_mask[HH_NL * HH_MW_MAX];
-    __shared__ uint16_t s_x[HH_NL];
-    __shared__ uint16_t s_n[HH_NL];
-    __shared__ uint8_t s_mem[HH_NL];
+    extern __shared__ __align__(16) uint8_t smem[];
+    __shared__ uint32_t s_ein[HH_NL];          // run entries pushed by walkers
+    __shared__ int16_t s_din[HH_NL];           // their deltas
+    __shared__ uint16_t s_exc[HH_NL];          // exception lanes (k > 1)
+    __shared__ uint8_t s_mem[HH_NL];           // live masks over entering d
     __shared__ uint8_t s_k[HH_NL];
-    __shared__ uint16_t s_exc[HH_NL];
-    __shared__ uint16_t s_ein[HH_NL];
-    __shared__ int16_t s_din[HH_NL];
-    __shared__ uint32_t s_cnt4[4];
-    __shared__ int32_t s_part[4][HH_KM];
-    __shared__ uint64_t s_out[HH_KM];
+    __shared__ int32_t s_part[HH_NL / 64][HH_KM];
+    __shared__ uint32_t s_ost[HH_KM];
     __shared__ uint64_t s_tab[HH_KM];
-    __shared__ uint64_t s_st[2];
-    __shared__ uint32_t s_tile;
-    extern __shared__ uint32_t s_l2[];
+    __shared__ int32_t s_tmp[HH_NL / 64];
+    __shared__ uint32_t s_cnt[HH_NL / 64];
+    __shared__ uint64_t s_bc[4];
 
-    const uint32_t lane = threadIdx.x;
-    const uint32_t mw = (S + 31) / 32;
-    const uint32_t span = (HH_NL + HH_KM + 1) * S + HH_SPAN_MARGIN;
-    const uint32_t nw = (span + 31) / 32 + 3;
-    stage_l1<HH_L1_SIZE>(s_l1, tab.l1);
-    for (uint32_t i = lane; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
+    uint64_t *s_l1 = (uint64_t *)smem;
+    uint32_t *s_w = (uint32_t *)(smem + HH_L1_SIZE * 8);
+    uint8_t *s_out = (uint8_t *)(s_w + SW * HH_NLS);
+    uint32_t *s_l2 = (uint32_t *)(s_out + geo.ob + 16);
+
+    const uint32_t j = threadIdx.x;
+    constexpr uint32_t S = 32 * SW;
+    const uint64_t tile_bits = (uint64_t)HH_NR * S;
+    const uint32_t span = HH_NCOL * S;          // bits staged per tile
     STAMP_DECL
 
-    // tiles A (to emit) and P (decoded last iteration): index and this
-    // lane's walk record
-    uint64_t tA = ~0ull, tP = ~0ull;
-    uint32_t aN = 0, aCov = 0, aE = 0, aK = 1;
-    int32_t aDel = 0;
-    uint32_t pN = 0, pCov = 0, pE = 0, pK = 1;
-    int32_t pDel = 0;
-    uint32_t *wB = s_w;                       // tile being decoded
-    uint32_t *wA = s_w + HH_NW_MAX;           // tile being emitted
+    for (uint32_t i = j; i < HH_L1_SIZE; i += HH_NL) s_l1[i] = tab.l1[i];
+    for (uint32_t i = j; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
 
-    for (;;) {
-        if (lane == 0) s_tile = atomicAdd(lb.counter, 1u);
+    uint64_t t = blockIdx.x;
+    Prefetch pf;
+    if (t < geo.ntiles) prefetch_tile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords, geo.vec4);
+
+    hh_ctx c;
+    c.w = s_w;
+    c.sw = SW;
+    c.magic = 0;
+    c.l1 = s_l1;
+    c.l2 = s_l2;
+    c.tree = tab.tree;
+    c.tsym = tab.tsym;
+
+    for (; t < geo.ntiles; t += gridDim.x) {
+        const uint64_t T0 = t * tile_bits;
+        const uint64_t rem = geo.bits - T0;
+        const uint32_t bt = rem < span ? (uint32_t)rem : span;
+        c.bt = bt;
+        __syncthreads();                 // previous tile done with s_w
+        store_tile<SW>(pf, s_w);
+        const uint64_t tn = t + gridDim.x;
+        if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
         __syncthreads();
-        const uint64_t tB = s_tile;
-        const bool hasB = tB < ntiles, hasA = tA < ntiles;
-        if (!hasA && !hasB && tP >= ntiles) break;
-        if (hasB) {
-            TSTAMP(tB, 0);
-#ifdef HH_STAMPS
-            if (lane == 0 && tB < HH_TDBG_MAX) dbg[gridDim.x * HH_NDBG + tB * 6 + 4] = blockIdx.x;
-#endif
-        }
-        uint64_t b0B = 0, b0A = 0;
-        uint32_t btB = 0, btA = 0;
-        Staged stg;
-        if (hasB) {
-            b0B = tB * (uint64_t)HH_NR * S;
-            const uint64_t rem = bits - b0B;
-            btB = rem < span ? (uint32_t)rem : span;
-            stage_load(stg, gdata, b0B >> 5, nw, nwords_ok);
-        }
-        if (hasA) {
-            b0A = tA * (uint64_t)HH_NR * S;
-            const uint64_t rem = bits - b0A;
-            btA = rem < span ? (uint32_t)rem : span;
-            Staged sa;
-            stage_load(sa, gdata, b0A >> 5, nw, nwords_ok);
-            stage_store(sa, wA, nw);
-        }
         STAMP(0);
 
-        // (2) tile A: entering state and output base
-        uint32_t pA = 0, peA = 0;
-        uintptr_t dst = 0;
-        if (hasA) {
-            TSTAMP(tA, 2);
-            if (lane < 64) {
-                uint64_t excl = 0, stw = 0;
-                bool ok = true;
-                uint32_t nrounds = 0, nspins = 0;
-                uint64_t lbd[4] = {0, 0, 0, 0};
-                if (tA > 0) ok = lookback_excl(lb, tA, flags, &excl, &nrounds, &nspins, lbd);
-                COUNT(8, lbd[0]);
-                COUNT(9, lbd[1]);
-                COUNT(10, lbd[2]);
-                COUNT(11, lbd[3]);
-                COUNT(6, nrounds + (ok ? 0ull : (1ull << 32)));
-                COUNT(7, nspins);
-                if (lane == 0) {
-                    if (tA > 0) {
-                        const uint64_t g = poll_granule(&lb.gran[tA - 1], flags);
-                        stw = (g & HH_GR_CST) ? gran_state(g) : (poll_granule(&lb.xst[tA - 1], flags) & HH_VAL_MASK);
-                        if (!ok) excl = poll_granule(&lb.incl[tA - 1], flags) & HH_VAL_MASK;
-                    }
-                    const uint64_t xf = ld_sc1(&lb.tabs[tA * HH_KM + (stw & 0xfu)]);
-                    const uint64_t incl = excl + (uint64_t)(int64_t)(int32_t)hh_xf_count(xf);
-                    st_sc1(&lb.xst[tA], xf_state(xf) | HH_GR_PUB);
-                    st_sc1(&lb.incl[tA], (incl & HH_VAL_MASK) | HH_INCL);
-                    if (tA == ntiles - 1) {
-                        flags[2] = (uint32_t)incl;
-                        flags[3] = (uint32_t)(incl >> 32);
-                    }
-                    s_st[0] = stw;
-                    s_st[1] = excl;
-                }
-            }
-            STAMP(1);
-            TSTAMP(tA, 3);
-            s_k[lane] = (uint8_t)aK;
-            __syncthreads();
-            const uint64_t sw = s_st[0];
-            const uint32_t din = (uint32_t)(sw & 0xfu);
-            s_mem[lane] = lane >= din && lane < HH_NR;
-            const uint32_t nexc = collect_exceptions(aK > 1 && lane < HH_NR, s_exc, s_cnt4);
-            if (lane == 0) {
-                for (uint32_t i = 0; i < nexc; i++) {
-                    const uint32_t j = s_exc[i], kj = s_k[j];
-                    if (!s_mem[j]) continue;
-                    for (uint32_t q = j + 1; q < j + kj && q < HH_NR; q++) s_mem[q] = 0;
-                }
-            }
-            __syncthreads();
-            const bool live = s_mem[lane] != 0;
-            if (live && lane + aK < HH_NR) {
-                s_ein[lane + aK] = (uint16_t)aE;
-                s_din[lane + aK] = (int16_t)aDel;
-            }
-            __syncthreads();
-            uint32_t e_in = 0;
-            int32_t del_in = 0;
-            if (live) {
-                e_in = lane == din ? (uint32_t)((sw >> 4) & 0xfffu) : s_ein[lane];
-                del_in = lane == din ? (int32_t)(int16_t)(uint16_t)(sw >> 16) : s_din[lane];
-            }
-            const uint32_t cnt = live ? (uint32_t)((int32_t)(aN + aCov) + del_in) : 0u;
-            uint32_t total;
-            const uint32_t off = block_excl_scan(cnt, s_cnt4, &total);
-            const uint64_t base = s_st[1] - (uint64_t)(int64_t)(int32_t)(int16_t)(uint16_t)(sw >> 16);
-            if (base + total > cap) {
-                if (lane == 0) atomicOr(flags, (uint32_t)F_OVER);
-            } else if (live) {
-                pA = lane * S + e_in;
-                const uint32_t end = (lane + aK) * S + aE;
-                peA = end < btA ? end : btA;
-                if (pA > peA) pA = peA;
-                dst = (uintptr_t)(out + base + off);
-            }
-            STAMP(2);
+        // pass 1: own region from offset 0
+        const uint32_t p0 = j * S;
+        uint32_t n = 0, x = bt;
+        if (p0 < bt) {
+            const uint32_t lim = p0 + S < bt ? p0 + S : bt;
+            x = hh_region_count(&c, p0, lim, &n);
         }
-        if (hasB) stage_store(stg, wB, nw);
-        __syncthreads();
+        STAMP(1);
 
-        // (3) B's region decode + A's emission, interleaved
-        hh_ctx cA, cB;
-        cA.w = wA; cA.sh = (uint32_t)(b0A & 31); cA.l1 = s_l1; cA.l2 = s_l2; cA.tree = tab.tree; cA.tsym = tab.tsym; cA.bt = btA;
-        cB.w = wB; cB.sh = (uint32_t)(b0B & 31); cB.l1 = s_l1; cB.l2 = s_l2; cB.tree = tab.tree; cB.tsym = tab.tsym;
-        cB.bt = btB;
-        const uint32_t p0 = lane * S;
-        uint32_t pB = p0, limB = p0, nB = 0, mbase = p0, wdone = 0;
-        uint64_t macc = 0;
-        if (hasB && p0 < btB) limB = p0 + S < btB ? p0 + S : btB;
-        uint64_t acc = 0;
-        uint32_t nacc = 0;
-        uint32_t *msk = &s_mask[lane * mw];
-        for (;;) {
-            const bool aB = pB < limB, aA = pA < peA;
-            if (!aB && !aA) break;
-            const uint32_t qB = pB + cB.sh, qA = pA + cA.sh;
-            const uint32_t b0 = wB[qB >> 5], b1 = wB[(qB >> 5) + 1];
-            const uint32_t a0 = wA[qA >> 5], a1 = wA[(qA >> 5) + 1];
-            const uint32_t winB = __builtin_amdgcn_alignbit(b1, b0, qB & 31);
-            const uint32_t winA = __builtin_amdgcn_alignbit(a1, a0, qA & 31);
-            const uint64_t eB = s_l1[winB & (HH_L1_SIZE - 1u)];
-            const uint64_t eA = s_l1[winA & (HH_L1_SIZE - 1u)];
-            if (aB) {
-                uint32_t ns = HH_L1_NSYM(eB), l, bm = 1u;
-                if (ns && pB + HH_L1_NBITS(eB) <= limB) {
-                    l = HH_L1_NBITS(eB);
-                    bm = HH_L1_BMASK(eB);
-                } else {
-                    if (ns) {
-                        l = HH_L1_LEN0(eB);
-                    } else {
-                        uint32_t s;
-                        l = hh_escape(&cB, pB, winB, eB, &s);
-                    }
-                    ns = 1;
-                }
-                macc |= (uint64_t)bm << (pB - mbase);
-                const uint32_t rem = btB - pB;
-                pB += l < rem ? l : rem;
-                nB += ns;
-                while (pB - mbase >= 32 && wdone < mw) {
-                    msk[wdone++] = (uint32_t)macc;
-                    macc >>= 32;
-                    mbase += 32;
-                }
-            }
-            if (aA) {
-                uint32_t ns = HH_L1_NSYM(eA), val, n, adv;
-                if (ns && pA + HH_L1_NBITS(eA) <= peA) {
-                    val = HH_L1_SYMS(eA);
-                    n = ns;
-                    adv = HH_L1_NBITS(eA);
-                } else {
-                    uint32_t s;
-                    if (ns) {
-                        adv = HH_L1_LEN0(eA);
-                        s = HH_L1_SYMS(eA) & 0xffu;
-                    } else {
-                        adv = hh_escape(&cA, pA, winA, eA, &s);
-                    }
-                    if (adv > btA - pA) {
-                        s = hh_tail_symbol(&cA, pA);
-                        adv = btA - pA;
-                    }
-                    val = s;
-                    n = 1;
-                }
-                acc |= (uint64_t)val << (8u * nacc);
-                nacc += n;
-                pA += adv;
-                if (nacc >= 4) {
-                    *(uint32_t *)dst = (uint32_t)acc;   // unaligned dword store (CDNA global memory)
-                    dst += 4;
-                    acc >>= 32;
-                    nacc -= 4;
-                }
+        // walks: region j's exit against the next regions' own chains
+        const hh_wk wk = hh_walk(&c, j, S, x);
+        if (wk.k == 0) {
+            // first failure: tile, lane, exit, count (hh_debug_failure)
+            atomicOr(flags, (uint32_t)F_FAIL);
+            if (atomicCAS(&flags[4], 0u, 1u) == 0u) {
+                flags[5] = (uint32_t)t; flags[6] = j; flags[7] = x; flags[8] = n; flags[9] = bt;
             }
         }
-        for (uint32_t i = 0; i < nacc; i++) *(uint8_t *)(dst + i) = (uint8_t)(acc >> (8 * i));
-        while (wdone < mw) {
-            msk[wdone++] = (uint32_t)macc;
-            macc >>= 32;
+        const uint32_t kk = wk.k ? wk.k : 1u;
+        s_k[j] = (uint8_t)kk;
+        s_mem[j] = (uint8_t)hh_mem_init(j);
+        STAMP(2);
+
+        // transfer table: live masks (exceptions, ascending, by one lane),
+        // charged count and leaving state for every entering d
+        const uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt);   // barriers inside
+        if (j == 0) {
+            for (uint32_t i = 0; i < nexc; i++) {
+                const uint32_t e = s_exc[i], ke = s_k[e];
+                const uint8_t m = s_mem[e];
+                for (uint32_t q = e + 1; q < e + ke && q < HH_NR; q++) s_mem[q] &= (uint8_t)~m;
+            }
         }
-        s_x[lane] = (uint16_t)(pB - p0);
-        s_n[lane] = (uint16_t)nB;
+        __syncthreads();
+        const uint32_t mem = s_mem[j];
+        const int32_t charged = (int32_t)(n + wk.cov) + wk.delta;
+        if (j + kk >= HH_NR) {
+            const uint32_t os = hh_state_pack(j + kk - HH_NR, wk.e, wk.delta);
+#pragma unroll
+            for (uint32_t d = 0; d < HH_KM; d++)
+                if ((mem >> d) & 1u) s_ost[d] = os;
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < HH_KM; d++) {
+            const int32_t v = wave_sum(((mem >> d) & 1u) ? charged : 0);
+            if ((j & 63u) == 0) s_part[j >> 6][d] = v;
+        }
+        __syncthreads();
+        if (j < HH_KM) {
+            int32_t cnt = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < HH_NL / 64; w++) cnt += s_part[w][j];
+            s_tab[j] = hh_tab_pack(cnt, s_ost[j]);
+        }
+        __syncthreads();
+        if (j == 0) {
+            // aggregate = table row d = 0; rows d >= 1 stay in LDS (a tile entered
+            // with d >= 1 publishes its inclusive prefix, look-backs wait for it)
+            bool cst = true;
+            for (uint32_t d = 1; d < HH_KM; d++) cst = cst && hh_tab_state(s_tab[d]) == hh_tab_state(s_tab[0]);
+            st_sc1(&lb.agg[t], HH_AGG | (cst ? HH_CST : 0ull) | s_tab[0]);
+            // state entering this tile
+            s_bc[0] = entering_state(lb, t, flags);
+        }
         __syncthreads();
         STAMP(3);
 
-        // (4) B's walks and transfer table
-        if (hasB) {
-            hh_rec r;
-            r.n = nB; r.k = 1; r.e = 0; r.delta = 0; r.cov = 0;
-            if (lane < HH_NR) {
-                hh_masks mk = {s_mask, s_x, s_n, HH_NL, mw};
-                hh_walk_mask(&cB, &mk, lane, S, pB, &r);
-                r.n = nB;
-                if (r.k == 0) atomicOr(flags, (uint32_t)F_FAIL);
-            }
-            const uint32_t kk = r.k ? r.k : 1u;
-            STAMP(4);
-            s_mem[lane] = lane >= HH_NR ? 0u : (lane >= HH_KM - 1 ? 0xffu : (uint8_t)((1u << (lane + 1)) - 1u));
-            s_k[lane] = (uint8_t)kk;
-            const uint32_t nexc = collect_exceptions(kk > 1 && lane < HH_NR, s_exc, s_cnt4);
-            if (lane == 0) {
-                for (uint32_t i = 0; i < nexc; i++) {
-                    const uint32_t j = s_exc[i], kj = s_k[j];
-                    const uint8_t m = s_mem[j];
-                    for (uint32_t q = j + 1; q < j + kj && q < HH_NR; q++) s_mem[q] &= (uint8_t)~m;
-                }
-            }
-            __syncthreads();
-            const uint32_t memd = s_mem[lane];
-            const int32_t contrib = lane < HH_NR ? (int32_t)(r.n + r.cov) + r.delta : 0;
-            if (lane < HH_NR && lane + kk >= HH_NR) {
-                for (uint32_t d = 0; d < HH_KM; d++)
-                    if ((memd >> d) & 1u) s_out[d] = hh_xf_pack(0, r.delta, r.e, lane + kk - HH_NR);
-            }
-#pragma unroll
-            for (uint32_t d = 0; d < HH_KM; d++) {
-                int32_t v = ((memd >> d) & 1u) ? contrib : 0;
-                v = (int32_t)wave_sum((uint32_t)v);
-                if ((lane & 63) == 0) s_part[lane >> 6][d] = v;
-            }
-            __syncthreads();
-            if (lane < HH_KM) {
-                const int32_t cnt = s_part[0][lane] + s_part[1][lane] + s_part[2][lane] + s_part[3][lane];
-                const uint64_t o = s_out[lane];
-                s_tab[lane] = hh_xf_pack((uint32_t)cnt, hh_xf_delta(o), hh_xf_e(o), hh_xf_d(o));
-            }
-            __syncthreads();
-            if (lane == 0) {
-                const uint64_t o0 = s_tab[0] >> 32;
-                bool cst = true;
-                for (uint32_t i = 0; i < HH_KM; i++) {
-                    st_sc1(&lb.tabs[tB * HH_KM + i], s_tab[i]);
-                    cst = cst && (s_tab[i] >> 32) == o0;
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_sc1(&lb.gran[tB], gran_pack(s_tab[0], cst));
-            }
-            TSTAMP(tB, 1);
-            STAMP(5);
-            // A <- P, P <- B
-            aN = pN; aCov = pCov; aE = pE; aK = pK; aDel = pDel;
-            pN = r.n; pCov = r.cov; pE = r.e; pK = kk; pDel = r.delta;
-        } else {
-            aN = pN; aCov = pCov; aE = pE; aK = pK; aDel = pDel;
+        // live lanes for the entering state, their run entries and offsets
+        const uint32_t st_in = (uint32_t)s_bc[0];
+        const uint32_t d_t = hh_state_d(st_in);
+        const int32_t dprev = hh_state_delta(st_in);
+        const bool live = (mem >> d_t) & 1u;
+        if (live && j + kk < HH_NR) {
+            s_ein[j + kk] = (j + kk) * S + wk.e;
+            s_din[j + kk] = (int16_t)wk.delta;
         }
-        tA = tP;
-        tP = hasB ? tB : ~0ull;
+        __syncthreads();
+        const uint32_t e_in = j == d_t ? d_t * S + hh_state_e(st_in) : s_ein[j];
+        const int32_t d_in = j == d_t ? dprev : (int32_t)s_din[j];
+        const uint32_t rc = live ? (uint32_t)((int32_t)(n + wk.cov) + d_in) : 0u;
+        int32_t Tout_i;
+        const uint32_t L = (uint32_t)block_excl_scan((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
+        const uint32_t Tout = (uint32_t)Tout_i;
+        const uint64_t tab_t = s_tab[d_t];
+        uint32_t p = live ? e_in : 0u;
+        const uint32_t y = (j + kk) * S + wk.e;
+        const uint32_t pe = live ? (y < bt ? y : bt) : 0u;
+        uint32_t o = L;
+        STAMP(4);
+
+        uint64_t P0 = 0;
+        for (uint32_t wlo = 0; wlo < Tout || wlo == 0; wlo += geo.ob) {
+            const uint32_t whi = wlo + geo.ob;
+            // pass 2: this lane's symbols with output index in [wlo, whi)
+            if (p < pe && o < whi) {
+                uint32_t val, k;
+                while ((o & 3u) && p < pe && o < whi) {        // head: align to a dword
+                    const uint32_t ha = (o + 3u) & ~3u;
+                    p += hh_emit_step(&c, p, pe, o, ha < whi ? ha : whi, &val, &k);
+                    for (uint32_t i = 0; i < k; i++) s_out[o - wlo + i] = (uint8_t)(val >> (8 * i));
+                    o += k;
+                }
+                uint64_t acc = 0;
+                uint32_t nacc = 0;
+                while (p < pe && o + nacc < whi) {
+                    p += hh_emit_step(&c, p, pe, o + nacc, whi, &val, &k);
+                    acc |= (uint64_t)val << (8 * nacc);
+                    nacc += k;
+                    if (nacc >= 4) {
+                        *(uint32_t *)(s_out + (o - wlo)) = (uint32_t)acc;
+                        acc >>= 32;
+                        nacc -= 4;
+                        o += 4;
+                    }
+                }
+                for (uint32_t i = 0; i < nacc; i++) s_out[o - wlo + i] = (uint8_t)(acc >> (8 * i));
+                o += nacc;
+            }
+            __syncthreads();
+            STAMP(5);
+
+            if (wlo == 0) {
+                // output base: decoupled look-back over the predecessors
+                if (j < 64) {
+                    const uint64_t excl = t > 0 ? lookback_excl(lb, t, flags) : 0ull;
+                    if (j == 0) {
+                        const uint64_t incl = excl + (uint64_t)(int64_t)hh_tab_count(tab_t);
+                        st_sc1(&lb.inc[t], hh_inc_pack(incl, hh_tab_state(tab_t)));
+                        const uint64_t base = excl - (uint64_t)(int64_t)dprev;
+                        s_bc[1] = base;
+                        if (t == geo.ntiles - 1) {
+                            const uint64_t tot = base + Tout;
+                            flags[2] = (uint32_t)tot;
+                            flags[3] = (uint32_t)(tot >> 32);
+                        }
+                        if (base + Tout > cap) atomicOr(flags, (uint32_t)F_OVER);
+                        if (lb.tdbg) {
+                            lb.tdbg[t * 8 + 0] = base;
+                            lb.tdbg[t * 8 + 1] = Tout | ((uint64_t)st_in << 32);
+                            lb.tdbg[t * 8 + 2] = excl;
+                            lb.tdbg[t * 8 + 3] = tab_t;
+                        }
+                    }
+                }
+                __syncthreads();
+                P0 = s_bc[1];
+                STAMP(6);
+            }
+
+            // copy the window to HBM: 16-B aligned chunks, ragged ends bytewise
+            const uint32_t nr = Tout - wlo < geo.ob ? Tout - wlo : geo.ob;
+            const uint64_t G = P0 + wlo;
+            if (G + nr <= cap && nr > 0) {
+                const uint64_t c0 = G >> 4, c1 = (G + nr + 15) >> 4;
+                for (uint64_t ch = c0 + j; ch < c1; ch += HH_NL) {
+                    const uint64_t a0 = ch << 4;
+                    if (a0 >= G && a0 + 16 <= G + nr) {
+                        const uint32_t s = (uint32_t)(a0 - G);
+                        const uint32_t *d = (const uint32_t *)(s_out + (s & ~3u));
+                        const uint32_t sh = (s & 3u) * 8u;
+                        const uint32_t w0 = d[0], w1 = d[1], w2 = d[2], w3 = d[3], w4 = d[4];
+                        u32x4 q;
+                        q.x = __builtin_amdgcn_alignbit(w1, w0, sh);
+                        q.y = __builtin_amdgcn_alignbit(w2, w1, sh);
+                        q.z = __builtin_amdgcn_alignbit(w3, w2, sh);
+                        q.w = __builtin_amdgcn_alignbit(w4, w3, sh);
+                        __builtin_nontemporal_store(q, (u32x4 *)(out + a0));
+                    } else {
+                        const uint64_t lo = a0 > G ? a0 : G;
+                        const uint64_t hi = a0 + 16 < G + nr ? a0 + 16 : G + nr;
+                        for (uint64_t a = lo; a < hi; a++) out[a] = s_out[a - G];
+                    }
+                }
+            }
+            STAMP(7);
+            if (wlo + geo.ob >= Tout) break;
+            __syncthreads();            // window copied before the next round
+        }
     }
     STAMP_FLUSH(dbg);
 }
@@ -733,6 +650,9 @@ __global__ void k_st_flag(const int32_t *steps, int64_t bits, int32_t step, int3
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
+typedef void (*kdec_t)(const uint32_t *, Geometry, DevTab, LookBack, uint8_t *, uint64_t, uint32_t *,
+                       uint64_t *);
+
 struct hh_decoder {
     int device;
     hh_config cfg;
@@ -745,6 +665,7 @@ struct hh_decoder {
     uint8_t *d_tsym;
     DevTab tab;
     uint32_t S;
+    uint32_t ob;
     // workspace
     void *ws;
     size_t ws_size;
@@ -752,8 +673,10 @@ struct hh_decoder {
     hipEvent_t ev[4];
     hh_stats stats;
     uint32_t grid;       // persistent grid size (occupancy x CUs)
-    size_t grid_l2b;     // dynamic LDS the grid was sized for
+    size_t grid_lds;     // dynamic LDS the grid was sized for
+    kdec_t grid_kf;      // and the kernel instance
     uint64_t *d_dbg;     // per-block phase cycles (HH_STAMPS builds)
+    uint64_t last_ntiles;
 };
 
 static int ensure_ws(hh_decoder *d, size_t need) {
@@ -775,13 +698,18 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
     if (cfg) d->cfg = *cfg;
     d->device = d->cfg.device;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || d->device >= ndev) {
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || d->device < 0 || d->device >= ndev) {
         free(d);
         return HH_ERR_DEVICE;
     }
     if (hipSetDevice(d->device) != hipSuccess) { free(d); return HH_ERR_DEVICE; }
     d->ht = (hh_tables *)calloc(1, sizeof(hh_tables));
     if (!d->ht) { free(d); return HH_ERR_NOMEM; }
+    d->ob = HH_OB_DEFAULT;
+    if (const char *e = getenv("HH_OB_KIB")) {
+        long v = strtol(e, nullptr, 10);
+        if (v >= 1 && v <= 96) d->ob = (uint32_t)v << 10;
+    }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&d->d_l1, sizeof(uint64_t) * HH_L1_SIZE) != hipSuccess ||
         hipMalloc(&d->d_l2, sizeof(uint32_t) * HH_L2_MAX) != hipSuccess ||
@@ -814,14 +742,14 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
 }
 
 static uint32_t pick_region_bits(const hh_tables *t, int req) {
-    if (req > 0) return (uint32_t)req;
-    // A region must hold a whole number of code-length periods, or chains
-    // of codes whose lengths share a factor (E.coli: all 2 bits) could never
-    // meet the true chain.  288 = 2^5 * 3^2 covers gcd 1,2,3,4,6,8,9,...
     uint32_t g = (uint32_t)(t->len_gcd > 0 ? t->len_gcd : 1);
-    if (HH_S_DEFAULT % g == 0) return HH_S_DEFAULT;
-    if (g <= HH_S_DEFAULT) return g * (HH_S_DEFAULT / g);
-    return g <= HH_S_MAX ? g : 0;
+    if (req > 0) {
+        // a requested size must keep whole words; off the code lattice it is
+        // still exact (walks that cannot merge report failure), only slower
+        if (req % 32 || req > 32 * HH_SW_MAX) return 0;
+        return (uint32_t)req;
+    }
+    return hh_pick_region_bits(g);
 }
 
 extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
@@ -857,19 +785,64 @@ static inline unsigned grid_for(int64_t n, unsigned bs) {
 }
 
 static int fast_path_ok(const hh_decoder *d) {
-    return d->S >= 32 && d->S <= HH_S_MAX && d->ht->maxlen <= HH_MAXLEN_FAST &&
+    return d->S >= 32 && d->S <= 32 * HH_SW_MAX && d->ht->maxlen <= HH_MAXLEN_FAST &&
            !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
 }
 
 static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8_t *d_out,
                           uint64_t cap, uint64_t *out_len, hipStream_t st);
 
+static size_t lds_bytes(const hh_decoder *d) {
+    return (size_t)HH_L1_SIZE * 8 + (size_t)(d->S / 32) * HH_NLS * 4 + d->ob + 16 +
+           (size_t)d->tab.l2_used * 4;
+}
+
+// k_decode instantiated per words-per-region (S = 32 * SW bits)
+static kdec_t kdec_for(uint32_t sw) {
+    switch (sw) {
+    case 1: return k_decode<1>;
+    case 2: return k_decode<2>;
+    case 3: return k_decode<3>;
+    case 4: return k_decode<4>;
+    case 5: return k_decode<5>;
+    case 6: return k_decode<6>;
+    case 7: return k_decode<7>;
+    case 8: return k_decode<8>;
+    case 9: return k_decode<9>;
+    case 10: return k_decode<10>;
+    case 11: return k_decode<11>;
+    case 12: return k_decode<12>;
+    default: return nullptr;
+    }
+}
+
+// Workgroups that can be resident at once (the persistent grid): the
+// occupancy answer, capped by the SGPR rule of MI355X_MICROARCH.md
+// ("Residency and cooperative launch") for one-block-per-CU-group sizing.
+static int size_grid(hh_decoder *d, size_t lds, kdec_t kf) {
+    if (d->grid && d->grid_lds == lds && d->grid_kf == kf) return HH_OK;
+    int per_cu = 0, ncu = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, HH_NL, lds));
+    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
+    if (per_cu < 1) return HH_ERR_UNSUPPORTED;
+    d->grid = (uint32_t)(per_cu * ncu);
+    d->grid_lds = lds;
+    d->grid_kf = kf;
+    if (d->d_dbg) HIP_OK(hipFree(d->d_dbg));
+    d->d_dbg = nullptr;
+    HIP_OK(hipMalloc(&d->d_dbg, (size_t)d->grid * HH_NDBG * sizeof(uint64_t)));
+    HIP_OK(hipMemset(d->d_dbg, 0, (size_t)d->grid * HH_NDBG * sizeof(uint64_t)));
+    return HH_OK;
+}
+
 extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits, void *d_out,
                                 uint64_t cap, uint64_t *out_len, void *hip_stream) {
     if (!d || !out_len || (!d_data && bits) || (!d_out && cap)) return HH_ERR_ARG;
     if (!d->have_tree) return HH_ERR_ARG;
     if (((uintptr_t)d_data & 3u) != 0) return HH_ERR_ARG;   // word loads
-    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : d->stream;
+    // NULL is the default stream (ordered with the caller's default-stream
+    // work, e.g. torch's), never the decoder's private non-blocking stream
+    hipStream_t st = (hipStream_t)hip_stream;
     HIP_OK(hipSetDevice(d->device));
     memset(&d->stats, 0, sizeof(d->stats));
     *out_len = 0;
@@ -878,44 +851,40 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
         d->stats.exact_fallback = 1;
         return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
     }
-    const uint32_t S = d->S;
-    const uint64_t tb = (uint64_t)HH_NR * S;
-    const uint64_t ntiles = (bits + tb - 1) / tb;
-    const uint64_t nwords_ok = ((bits + 7) / 8 + HH_PAYLOAD_PAD) / 4;
-    // workspace: [flags 64 B | counter, gran, incl, xst (zeroed) | tables]
-    const size_t zero_bytes = (16 + ntiles * 24 + 15) & ~(size_t)15;
-    size_t need = 64 + zero_bytes + ntiles * HH_KM * 8 + 256;
-    int rc = ensure_ws(d, need);
+    Geometry geo;
+    geo.bits = bits;
+    geo.S = d->S;
+    geo.sw = d->S / 32;
+    geo.magic = hh_magic(geo.sw);
+    geo.ob = d->ob;
+    geo.nwords = ((bits + 7) / 8 + HH_PAYLOAD_PAD) / 4;
+    const uint64_t tb = (uint64_t)HH_NR * d->S;
+    geo.ntiles = (bits + tb - 1) / tb;
+    geo.vec4 = (((uintptr_t)d_data & 15u) == 0) && (geo.sw % 4 == 0);
+    // workspace: [flags 64 B | agg[ntiles] | inc[ntiles]] (zeroed)
+    //            | (HH_DEBUG_TILES) tdbg[ntiles][8]
+    const size_t zero_bytes = 64 + (size_t)geo.ntiles * 16;
+    const int dbg_tiles = getenv("HH_DEBUG_TILES") != nullptr;
+    int rc = ensure_ws(d, zero_bytes + (size_t)geo.ntiles * (dbg_tiles ? 8 : 0) * 8 + 256);
     if (rc) return rc;
     uint8_t *w = (uint8_t *)d->ws;
     uint32_t *d_flags = (uint32_t *)w;
     LookBack lb;
-    lb.counter = (uint32_t *)(w + 64);
-    lb.gran = (uint64_t *)(w + 64 + 16);
-    lb.incl = lb.gran + ntiles;
-    lb.xst = lb.incl + ntiles;
-    lb.tabs = (uint64_t *)(w + 64 + zero_bytes);
-    const size_t l2b = sizeof(uint32_t) * d->tab.l2_used;
-    if (!d->grid || d->grid_l2b != l2b) {
-        int per_cu = 0, ncu = 0;
-        HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode, HH_NL, l2b));
-        d->grid_l2b = l2b;
-        if (d->d_dbg) HIP_OK(hipFree(d->d_dbg));
-        HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
-        d->grid = (uint32_t)((per_cu > 0 ? per_cu : 1) * ncu);
-        size_t dbg_words = (size_t)d->grid * HH_NDBG;
-#ifdef HH_STAMPS
-        dbg_words += (size_t)HH_TDBG_MAX * 6;
-#endif
-        HIP_OK(hipMalloc(&d->d_dbg, dbg_words * sizeof(uint64_t)));
-        HIP_OK(hipMemset(d->d_dbg, 0, dbg_words * sizeof(uint64_t)));
-    }
-    const uint32_t grid = (uint32_t)(ntiles < d->grid ? ntiles : d->grid);
+    lb.agg = (uint64_t *)(w + 64);
+    lb.inc = lb.agg + geo.ntiles;
+    lb.tdbg = dbg_tiles ? lb.inc + geo.ntiles : nullptr;
+    d->last_ntiles = geo.ntiles;
+    const size_t lds = lds_bytes(d);
+    const kdec_t kf = kdec_for(geo.sw);
+    if (!kf) return HH_ERR_UNSUPPORTED;
+    rc = size_grid(d, lds, kf);
+    if (rc) return rc;
+    const uint32_t grid = (uint32_t)(geo.ntiles < d->grid ? geo.ntiles : d->grid);
 
-    HIP_OK(hipMemsetAsync(d_flags, 0, 64 + zero_bytes, st));
+    HIP_OK(hipMemsetAsync(d_flags, 0, zero_bytes, st));
     HIP_OK(hipEventRecord(d->ev[0], st));
-    hipLaunchKernelGGL(k_decode, dim3(grid), dim3(HH_NL), l2b, st, (const uint32_t *)d_data, bits,
-                       nwords_ok, S, d->tab, ntiles, lb, (uint8_t *)d_out, cap, d_flags, d->d_dbg);
+    hipLaunchKernelGGL(kf, dim3(grid), dim3(HH_NL), lds, st, (const uint32_t *)d_data, geo,
+                       d->tab, lb, (uint8_t *)d_out, cap, d_flags, d->d_dbg);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d->ev[1], st));
     HIP_OK(hipMemcpyAsync(d->h_flags, d_flags, 16, hipMemcpyDeviceToHost, st));
@@ -925,20 +894,19 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     float ms = 0;
     hipEventElapsedTime(&ms, d->ev[0], d->ev[1]);
     d->stats.ms_total = ms;
-    d->stats.ms_sync = 0;
-    d->stats.ms_scan = 0;
     d->stats.ms_emit = ms;
-    d->stats.lanes = ntiles * HH_NR;
+    d->stats.lanes = geo.ntiles * HH_NR;
     d->stats.out_len = total;
     if (fl & F_TIMEOUT) return HH_ERR_TIMEOUT;
     if (fl & F_FAIL) {
-        // A walk found no shared boundary within HH_KM regions: the code does
-        // not resynchronise (non-synchronising code) -- take the exact path.
+        // A walk found no shared boundary inside the next region (a code that
+        // does not resynchronise within S bits): take the exact path.
         d->stats.exact_fallback = 1;
+        d->stats.repairs = 1;
         return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
     }
     *out_len = total;
-    if (total > cap) return HH_ERR_CAPACITY;
+    if (total > cap || (fl & F_OVER)) return HH_ERR_CAPACITY;
     return HH_OK;
 }
 
@@ -1098,28 +1066,36 @@ extern "C" int hh_stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits
                                  uint64_t cap, uint64_t *out_len, void *s) {
     if (!d || !d->have_tree || !out_len) return HH_ERR_ARG;
     HIP_OK(hipSetDevice(d->device));
-    hipStream_t st = s ? (hipStream_t)s : d->stream;
+    hipStream_t st = (hipStream_t)s;   // NULL = the default stream
     return stage_pipeline(d, d_data, bits, d_out, cap, out_len, st);
+}
+
+// Diagnostic: the first failed walk of the last decode (tile, lane, exit,
+// count, tile end); 0 if none.
+extern "C" int hh_debug_failure(hh_decoder *d, uint32_t *out5) {
+    if (!d || !out5 || !d->ws) return 0;
+    uint32_t f[10];
+    if (hipMemcpy(f, d->ws, sizeof(f), hipMemcpyDeviceToHost) != hipSuccess) return HH_ERR_DEVICE;
+    for (int i = 0; i < 5; i++) out5[i] = f[5 + i];
+    return (int)f[4];
+}
+
+// Diagnostic (HH_DEBUG_TILES set at decode time): per-tile [base, size |
+// entering state << 32, exclusive charged prefix, table entry, look-back's
+// inclusive tile, its prefix, counts summed, rounds] of the last
+// decode.  Returns the number of tiles written.
+extern "C" int hh_debug_tiles(hh_decoder *d, uint64_t *out, int max_tiles) {
+    if (!d || !out || !d->ws || !getenv("HH_DEBUG_TILES")) return 0;
+    const uint64_t nt = d->last_ntiles;
+    const int n = (int)(nt < (uint64_t)max_tiles ? nt : (uint64_t)max_tiles);
+    const uint64_t *src = (const uint64_t *)((uint8_t *)d->ws + 64) + nt * 2;
+    if (hipMemcpy(out, src, (size_t)n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return HH_ERR_DEVICE;
+    return n;
 }
 
 // Diagnostic: per-block phase cycle sums of the last decode (HH_STAMPS
 // builds; zeros otherwise).  Returns the number of blocks written.
-// Diagnostic builds only: per-tile global timestamps (s_memrealtime, 100 MHz)
-// [grab, granule published, look-back start, look-back end, block, -].
-extern "C" int hh_debug_tile_times(hh_decoder *d, uint64_t *out, int max_tiles) {
-#ifdef HH_STAMPS
-    if (!d || !out || !d->d_dbg) return 0;
-    int n = max_tiles < (int)HH_TDBG_MAX ? max_tiles : (int)HH_TDBG_MAX;
-    if (hipMemcpy(out, d->d_dbg + (size_t)d->grid * HH_NDBG, (size_t)n * 6 * sizeof(uint64_t),
-                  hipMemcpyDeviceToHost) != hipSuccess)
-        return 0;
-    return n;
-#else
-    (void)d; (void)out; (void)max_tiles;
-    return 0;
-#endif
-}
-
 extern "C" int hh_debug_phase_cycles(hh_decoder *d, uint64_t *out, int max_blocks) {
     if (!d || !out || !d->d_dbg) return 0;
     int n = (int)d->grid < max_blocks ? (int)d->grid : max_blocks;

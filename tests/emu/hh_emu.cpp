@@ -1,162 +1,235 @@
-// hh_emu.cpp -- TEST-ONLY host emulation of the fused decode kernel.
+// hh_emu.cpp -- TEST-ONLY host emulation of the decode kernel.
 //
 // Runs the kernel's per-lane building blocks (hh_algo.h) on host arrays with
-// the kernel's geometry -- tiles of HH_NL-1 regions, one auxiliary lane that
-// decodes the next tile's first region, boundary masks, mask walks, tile
-// transfer tables, ordered state application, the look-back's charged
-// counts, emission -- so the stitching
-// logic is checked against the oracle without a GPU.  Every lane's mask walk
-// is also cross-checked against the plain two-pointer walk.  Nothing in the
-// product links this file; it builds into tests/emu/libhh_emu.so.
+// the kernel's geometry and LDS layout -- tiles of HH_NR regions staged as
+// transposed word columns (plus HH_KM regions of the next tile), two-pointer
+// walks across up to HH_KM regions, live masks and exceptions, the tile
+// transfer table over the entering state, the resolved state chain between
+// tiles and per-lane emission at the kernel's local offsets -- so the
+// stitching logic is checked against the oracle without a GPU.  Every lane's
+// emitted run is checked against its predicted count, every tile's output
+// size against its table entry and every tile's base against the charged
+// prefix.  Nothing in the product links this file; it builds into
+// tests/emu/libhh_emu.so.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "hh_algo.h"
 #include "hiphuff.h"
 
+static uint32_t g_ob = 0;   // > 0: also replay the kernel's windowed pass 2
+
 extern "C" {
 
-// stats[0]=tiles stats[1]=walks with k>1 stats[2]=failed walks stats[3]=max k
+void hh_emu_set_window(uint32_t ob) { g_ob = ob; }
+
+// stats[0]=tiles stats[1]=walks with k > 1 stats[2]=failed walks
+// stats[3]=region bits used stats[4]=max k stats[5]=non-CONST tiles
 int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *sym,
                       int32_t nodes, const uint8_t *data, uint64_t bits, uint32_t S,
                       uint8_t *out, uint64_t cap, int64_t *stats) {
-    const uint32_t NR = HH_NL - 1;
     hh_tree tree = {nodes, izero, ione, sym};
     static hh_tables T;   // large; not reentrant (test helper)
     int rc = hh_tables_build(&tree, &T);
     if (rc) return rc;
-    for (int i = 0; i < 4; i++) stats[i] = 0;
+    for (int i = 0; i < 6; i++) stats[i] = 0;
+    if (S == 0) S = hh_pick_region_bits((uint32_t)T.len_gcd);
+    stats[3] = S;
     if (bits == 0) return 0;
-    if (S < 2 || S > 32 * HH_MW_MAX) return HH_ERR_ARG;
-    const uint64_t TB = (uint64_t)NR * S;
+    if (S < 32 || S % 32 || S > 32 * HH_SW_MAX) return HH_ERR_ARG;
+    const uint32_t sw = S / 32;
+    const uint64_t TB = (uint64_t)HH_NR * S;
     const uint64_t ntiles = (bits + TB - 1) / TB;
     const uint64_t nbytes = (bits + 7) / 8;
-    const uint32_t span = (HH_NL + HH_KM + 1) * S + 320;  // bits a tile may touch
-    const uint32_t nw = span / 32 + 3;
-    const uint32_t mw = (S + 31) / 32;
-    std::vector<uint32_t> w(nw);
-    std::vector<uint64_t> rec((size_t)ntiles * NR), tab((size_t)ntiles * HH_KM);
-    std::vector<uint32_t> mask(HH_NL * mw);
-    std::vector<uint16_t> mx(HH_NL), mn(HH_NL);
-    std::vector<uint32_t> xs(HH_NL), ns(HH_NL);
+    const uint32_t span = HH_NCOL * S;
+    std::vector<uint32_t> w((size_t)sw * HH_NLS);
+    std::vector<uint32_t> xs(HH_NR), ns(HH_NR), mem(HH_NR), ent(HH_NR);
+    std::vector<int32_t> din(HH_NR);
+    std::vector<hh_wk> wk(HH_NR);
     stats[0] = (int64_t)ntiles;
 
-    auto load_tile = [&](uint64_t t, hh_ctx &c) {
-        uint64_t b0 = t * TB;
-        uint64_t w0 = b0 >> 5;
-        for (uint32_t i = 0; i < nw; i++) {
-            uint64_t byte = (w0 + i) * 4;
-            uint32_t v = 0;
-            for (int k = 0; k < 4; k++)
-                if (byte + k < nbytes) v |= (uint32_t)data[byte + k] << (8 * k);
-            w[i] = v;
+    auto word_at = [&](uint64_t gw) -> uint32_t {
+        uint32_t v = 0;
+        for (int k = 0; k < 4; k++) {
+            uint64_t byte = gw * 4 + k;
+            if (byte < nbytes) v |= (uint32_t)data[byte] << (8 * k);
         }
+        return v;
+    };
+
+    uint64_t base = 0;                            // P_0 of the tile
+    int64_t excl = 0;                             // charged prefix of tiles < t
+    uint32_t st_in = hh_state_pack(0, 0, 0);      // resolved entering state
+    for (uint64_t t = 0; t < ntiles; t++) {
+        hh_ctx c;
+        const uint64_t tw0 = t * TB / 32;
+        for (uint32_t col = 0; col < HH_NCOL; col++)          // the kernel's staging
+            for (uint32_t k = 0; k < sw; k++) w[k * HH_NLS + col] = word_at(tw0 + (uint64_t)col * sw + k);
         c.w = w.data();
-        c.sh = (uint32_t)(b0 & 31);
+        c.sw = sw;
+        c.magic = hh_magic(sw);
         c.l1 = T.l1;
         c.l2 = T.l2;
         c.tree = T.tree;
         c.tsym = T.tsym;
-        uint64_t rem = bits - b0;
+        const uint64_t rem = bits - t * TB;
         c.bt = rem < span ? (uint32_t)rem : span;
-    };
+        const uint32_t bt = c.bt;
 
-    for (uint64_t t = 0; t < ntiles; t++) {
-        hh_ctx c;
-        load_tile(t, c);
-        for (uint32_t lane = 0; lane < HH_NL; lane++) {   // incl. the aux lane
-            uint32_t p0 = lane * S;
-            uint32_t n = 0, x = p0, n2 = 0;
-            struct MS {
-                uint32_t *m;
-                void operator()(uint32_t wi, uint32_t v) { m[wi] = v; }
-            } ms{&mask[lane * mw]};
-            for (uint32_t w2 = 0; w2 < mw; w2++) mask[lane * mw + w2] = 0;
-            if (p0 < c.bt) {
-                x = hh_region_count(&c, p0, p0 + S, &n);
-                uint32_t x2 = hh_region_count_mask(&c, p0, p0 + S, mw, &n2, ms);
-                if (x2 != x || n2 != n) return HH_ERR_INTERNAL;
+        for (uint32_t j = 0; j < HH_NR; j++) {            // pass 1
+            uint32_t p0 = j * S, n = 0, x = bt;
+            if (p0 < bt) {
+                uint32_t lim = p0 + S < bt ? p0 + S : bt;
+                x = hh_region_count(&c, p0, lim, &n);
             }
-            xs[lane] = x;
-            ns[lane] = n;
-            mx[lane] = (uint16_t)(x - p0);
-            mn[lane] = (uint16_t)n;
+            xs[j] = x;
+            ns[j] = n;
         }
-        hh_masks mk = {mask.data(), mx.data(), mn.data(), HH_NL, mw};
-        for (uint32_t lane = 0; lane < NR; lane++) {
-            hh_rec r, r2;
-            hh_walk(&c, lane, S, xs[lane], &r);
-            hh_walk_mask(&c, &mk, lane, S, xs[lane], &r2);
-            if (r.k != r2.k || r.e != r2.e || r.delta != r2.delta || r.cov != r2.cov) {
-                fprintf(stderr, "walk mismatch tile %lu lane %u: 2ptr k=%u e=%u d=%d cov=%u | mask k=%u e=%u d=%d cov=%u\n",
-                        (unsigned long)t, lane, r.k, r.e, r.delta, r.cov, r2.k, r2.e, r2.delta, r2.cov);
-                return HH_ERR_INTERNAL - 100;
-            }
-            r2.n = ns[lane];
-            if (r2.k == 0) stats[2]++;
-            if (r2.k > 1) stats[1]++;
-            if ((int64_t)r2.k > stats[3]) stats[3] = r2.k;
-            rec[t * NR + lane] = hh_rec_pack(r2);
+        for (uint32_t j = 0; j < HH_NR; j++) {            // walks
+            wk[j] = hh_walk(&c, j, S, xs[j]);
+            if (wk[j].k == 0) stats[2]++;
+            if (wk[j].k > 1) stats[1]++;
+            if ((int64_t)wk[j].k > stats[4]) stats[4] = wk[j].k;
         }
-        hh_tile_table_seq(&rec[t * NR], NR, &tab[t * HH_KM]);
-    }
-    if (stats[2]) return HH_ERR_UNSUPPORTED;
-
-    // ordered application of the tile tables (the kernel's look-back)
-    std::vector<hh_state> st(ntiles + 1);
-    st[0] = hh_state{0, 0, 0, 0};
-    for (uint64_t t = 0; t < ntiles; t++) st[t + 1] = hh_xf_apply(&tab[t * HH_KM], st[t]);
-    uint64_t total = st[ntiles].base;
-    if (total > cap) return HH_ERR_CAPACITY;
-
-    // The kernel's look-back sums CHARGED counts (each walk's delta charged
-    // to the walker's tile: count_t(d) = sum over live lanes of n+cov+delta)
-    // and starts tile t's first run delta_in(t) symbols before that prefix.
-    {
-        int64_t charged = 0;
-        for (uint64_t t = 0; t < ntiles; t++) {
-            if ((int64_t)st[t].base != charged - st[t].delta) return HH_ERR_INTERNAL - 200;
-            for (uint32_t j = st[t].d; j < NR;) {
-                hh_rec r = hh_rec_unpack(rec[t * NR + j]);
-                charged += (int64_t)r.n + r.cov + r.delta;
-                j = hh_rec_next(j, r);
+        if (stats[2]) return HH_ERR_UNSUPPORTED;
+        // transfer table
+        for (uint32_t j = 0; j < HH_NR; j++) mem[j] = hh_mem_init(j);
+        for (uint32_t j = 0; j < HH_NR; j++)              // exceptions, ascending
+            for (uint32_t q = j + 1; q < j + wk[j].k && q < HH_NR; q++) mem[q] &= ~mem[j];
+        int32_t cnt[HH_KM];
+        uint32_t ost[HH_KM];
+        int nlast[HH_KM];
+        for (uint32_t d = 0; d < HH_KM; d++) { cnt[d] = 0; nlast[d] = 0; ost[d] = 0; }
+        for (uint32_t j = 0; j < HH_NR; j++) {
+            const int32_t ch = (int32_t)(ns[j] + wk[j].cov) + wk[j].delta;
+            for (uint32_t d = 0; d < HH_KM; d++) {
+                if (!((mem[j] >> d) & 1u)) continue;
+                cnt[d] += ch;
+                if (j + wk[j].k >= HH_NR) {
+                    ost[d] = hh_state_pack(j + wk[j].k - HH_NR, wk[j].e, wk[j].delta);
+                    nlast[d]++;
+                }
             }
         }
-        if (charged != (int64_t)total) return HH_ERR_INTERNAL - 201;
-    }
-
-    struct Sink {
-        uint8_t *out;
-        void operator()(uint64_t o, uint32_t b) { out[o] = (uint8_t)b; }
-    } sink{out};
-    for (uint64_t t = 0; t < ntiles; t++) {
-        hh_ctx c;
-        load_tile(t, c);
-        hh_state s = st[t];
-        uint32_t j = s.d, e_in = s.e;
-        int32_t del_in = s.delta;
-        uint64_t o = s.base;
-        while (j < NR) {
-            hh_rec r = hh_rec_unpack(rec[t * NR + j]);
-            uint32_t nx = hh_rec_next(j, r);
-            uint32_t start = j * S + e_in, end = nx * S + r.e;
-            uint32_t pe = end < c.bt ? end : c.bt;
-            uint64_t cnt = (uint64_t)((int64_t)r.n + r.cov + del_in);
-            uint32_t p = start;
-            uint64_t o0 = o;
-            if (p < pe) hh_emit_run(&c, &p, pe, &o, total, sink);
-            if (o - o0 != cnt) return HH_ERR_INTERNAL;   // count/emission disagree
-            e_in = r.e;
-            del_in = r.delta;
-            j = nx;
+        bool cst = true;
+        for (uint32_t d = 0; d < HH_KM; d++) {
+            if (nlast[d] != 1) return HH_ERR_INTERNAL - 400;
+            if (hh_tab_state(hh_tab_pack(cnt[d], ost[d])) != ost[d] ||
+                hh_tab_count(hh_tab_pack(cnt[d], ost[d])) != cnt[d])
+                return HH_ERR_INTERNAL - 401;                // field overflow
+            if (ost[d] != ost[0]) cst = false;
         }
-        if (o != st[t + 1].base) return HH_ERR_INTERNAL;
+        if (!cst) stats[5]++;
+        // entering state -> live lanes, entries, run counts
+        const uint32_t d_t = hh_state_d(st_in), e_t = hh_state_e(st_in);
+        const int32_t dprev = hh_state_delta(st_in);
+        if ((int64_t)base != excl - dprev) return HH_ERR_INTERNAL - 300;
+        for (uint32_t j = 0; j < HH_NR; j++) { ent[j] = 0; din[j] = 0; }
+        ent[d_t] = d_t * S + e_t;
+        din[d_t] = dprev;
+        for (uint32_t j = 0; j < HH_NR; j++)
+            if (((mem[j] >> d_t) & 1u) && j + wk[j].k < HH_NR) {
+                ent[j + wk[j].k] = (j + wk[j].k) * S + wk[j].e;
+                din[j + wk[j].k] = wk[j].delta;
+            }
+        uint64_t o = base;
+        for (uint32_t j = 0; j < HH_NR; j++) {            // emission
+            if (!((mem[j] >> d_t) & 1u)) continue;
+            const uint32_t pe0 = (j + wk[j].k) * S + wk[j].e;
+            const uint32_t pe = pe0 < bt ? pe0 : bt;
+            const uint64_t want = (uint64_t)((int64_t)ns[j] + wk[j].cov + din[j]);
+            uint32_t p = ent[j];
+            const uint64_t o0 = o;
+            while (p < pe) {
+                uint32_t val, k;
+                p += hh_emit_step(&c, p, pe, o, ~0ull, &val, &k);
+                for (uint32_t i = 0; i < k; i++) {
+                    if (o + i >= cap) return HH_ERR_CAPACITY;
+                    out[o + i] = (uint8_t)(val >> (8 * i));
+                }
+                o += k;
+            }
+            if (o - o0 != want || (p != pe && !(p >= pe && ent[j] >= pe))) {
+                fprintf(stderr, "emu: tile %lu lane %u emitted %lu, predicted %lu (e=%u pe=%u p=%u)\n",
+                        (unsigned long)t, j, (unsigned long)(o - o0), (unsigned long)want, ent[j], pe, p);
+                return HH_ERR_INTERNAL;
+            }
+        }
+        const uint32_t so = ost[d_t];
+        const int64_t tout = (int64_t)cnt[d_t] - hh_state_delta(so) + dprev;
+        if (getenv("HH_EMU_TILE") && (uint64_t)atoll(getenv("HH_EMU_TILE")) == t) {
+            fprintf(stderr, "tile %lu: in 0x%x base %lu excl %ld cnt0 %d out0 0x%x tout %ld\n",
+                    (unsigned long)t, st_in, (unsigned long)base, (long)excl, cnt[0], ost[0], (long)tout);
+            for (uint32_t j = HH_NR - 10; j < HH_NR; j++)
+                fprintf(stderr, "  lane %u n %u x %u k %u e %u cov %u delta %d mem %x\n", j, ns[j], xs[j],
+                        wk[j].k, wk[j].e, wk[j].cov, wk[j].delta, mem[j]);
+        }
+        if ((int64_t)(o - base) != tout) return HH_ERR_INTERNAL - 2;
+        if (g_ob) {
+            // the kernel's pass 2 exactly: per-lane (p, o) carried across
+            // output windows of g_ob bytes, head bytes to a dword boundary,
+            // dword writes, tail bytes; then the window copy
+            std::vector<uint32_t> P(HH_NR), PE(HH_NR), OO(HH_NR);
+            uint32_t L = 0;
+            for (uint32_t j = 0; j < HH_NR; j++) {
+                const bool live = (mem[j] >> d_t) & 1u;
+                const uint32_t y = (j + wk[j].k) * S + wk[j].e;
+                P[j] = live ? ent[j] : 0u;
+                PE[j] = live ? (y < bt ? y : bt) : 0u;
+                OO[j] = L;
+                L += live ? (uint32_t)((int64_t)ns[j] + wk[j].cov + din[j]) : 0u;
+            }
+            std::vector<uint8_t> win(g_ob + 16);
+            for (uint32_t wlo = 0; wlo < L || wlo == 0; wlo += g_ob) {
+                const uint32_t whi = wlo + g_ob;
+                std::fill(win.begin(), win.end(), 0xAB);
+                for (uint32_t j = 0; j < HH_NR; j++) {
+                    uint32_t &p = P[j], &oo = OO[j];
+                    const uint32_t pe = PE[j];
+                    if (!(p < pe && oo < whi)) continue;
+                    uint32_t val, k;
+                    while ((oo & 3u) && p < pe && oo < whi) {
+                        const uint32_t ha = (oo + 3u) & ~3u;
+                        p += hh_emit_step(&c, p, pe, oo, ha < whi ? ha : whi, &val, &k);
+                        for (uint32_t i = 0; i < k; i++) win[oo - wlo + i] = (uint8_t)(val >> (8 * i));
+                        oo += k;
+                    }
+                    uint64_t acc = 0;
+                    uint32_t nacc = 0;
+                    while (p < pe && oo + nacc < whi) {
+                        p += hh_emit_step(&c, p, pe, oo + nacc, whi, &val, &k);
+                        acc |= (uint64_t)val << (8 * nacc);
+                        nacc += k;
+                        if (nacc >= 4) {
+                            memcpy(&win[oo - wlo], &acc, 4);
+                            acc >>= 32;
+                            nacc -= 4;
+                            oo += 4;
+                        }
+                    }
+                    for (uint32_t i = 0; i < nacc; i++) win[oo - wlo + i] = (uint8_t)(acc >> (8 * i));
+                    oo += nacc;
+                }
+                const uint32_t nr = L - wlo < g_ob ? L - wlo : g_ob;
+                for (uint32_t i = 0; i < nr; i++)
+                    if (win[i] != out[base + wlo + i]) {
+                        fprintf(stderr, "emu: window mismatch tile %lu byte %u (window %u)\n",
+                                (unsigned long)t, wlo + i, wlo);
+                        return HH_ERR_INTERNAL - 3;
+                    }
+                if (wlo + g_ob >= L) break;
+            }
+        }
+        excl += cnt[d_t];
+        base = o;
+        st_in = so;
     }
-    return (int64_t)total;
+    return (int64_t)base;
 }
 
 }  // extern "C"

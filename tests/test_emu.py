@@ -1,11 +1,12 @@
 """The fast path's stitching algorithm (hh_algo.h, exactly as the kernel runs
-it, tile by tile) emulated on the host and checked against the oracle.
+it, tile by tile, on the kernel's transposed LDS layout) emulated on the
+host and checked against the oracle.
 
-Covers the reference fixtures at several region sizes (tiny regions force
-many multi-region walks, k up to HH_KM), random trees and streams, codes cut
-off by the end of the stream (the reference's tail rule), and
-non-synchronising codes (the walk must report failure, never a wrong
-answer)."""
+Covers the reference fixtures at the default and a small region size, random
+trees and streams, codes cut off by the end of the stream (the reference's
+tail rule), fixed-length codes (region sizes on the code lattice merge at
+once) and non-synchronising region sizes (the walks must report failure,
+never a wrong answer)."""
 import ctypes as C
 import os
 
@@ -39,7 +40,7 @@ def run_emu(emu, izero, ione, sym, data, bits, S):
     d = np.zeros((bits + 7) // 8 + 64, np.uint8)
     d[: (bits + 7) // 8] = np.asarray(data, np.uint8)[: (bits + 7) // 8]
     out = np.zeros(bits + 16, np.uint8)
-    st = np.zeros(4, np.int64)
+    st = np.zeros(6, np.int64)
     n = emu.hh_emu_decode(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), d.ctypes.data,
                           bits, S, out.ctypes.data, len(out), st.ctypes.data)
     return n, out[: max(n, 0)], st
@@ -53,15 +54,15 @@ def oracle_chain(izero, ione, sym, data, bits):
 
 @pytest.mark.parametrize("name", ["hello", "paper1", "news", "book2", "kjv.txt", "E.coli",
                                   "world192.txt", "bible.txt"])
-@pytest.mark.parametrize("S", [288, 96])
+@pytest.mark.parametrize("S", [0, 96])
 def test_fixtures(emu, name, S):
     hf = H.HuffFile.load(os.path.join(FILES, name + ".huff"))
     ref = O.OracleHuff.load(os.path.join(FILES, name + ".huff")).chain_decode()
     n, out, st = run_emu(emu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits, S)
-    if n == UNSUPPORTED:          # only acceptable as a detected failure
-        assert st[2] > 0
+    if S and n == UNSUPPORTED:    # small regions: runs longer than HH_KM regions
+        assert st[2] > 0          # are detected, never mis-decoded
         return
-    assert n == len(ref) and np.array_equal(out, ref)
+    assert n == len(ref) and np.array_equal(out, ref), (n, st)
 
 
 def random_tree(rng, nleaves):
@@ -94,7 +95,8 @@ def test_random_trees_and_tails(emu, seed):
     data, bits = t.encode(text)
     for cut in (bits, bits - 1, max(1, bits // 3 + 1)):   # cut codes exercise the tail rule
         ref = oracle_chain(iz, io, sy, data, cut)
-        for S in (288, 64):
+        g = t.info()["len_gcd"]
+        for S in (0, 64 if 64 % g == 0 else 0):
             n, out, st = run_emu(emu, iz, io, sy, data, cut, S)
             if n == UNSUPPORTED:
                 assert st[2] > 0
@@ -105,7 +107,7 @@ def test_random_trees_and_tails(emu, seed):
 
 def test_empty_stream(emu):
     hf = H.HuffFile.load(os.path.join(FILES, "hello.huff"))
-    n, out, st = run_emu(emu, hf.izero, hf.ione, hf.sym, hf.payload, 0, 288)
+    n, out, st = run_emu(emu, hf.izero, hf.ione, hf.sym, hf.payload, 0, 0)
     assert n == 0
 
 
@@ -125,29 +127,47 @@ def complete_tree(depth):
     return np.array(iz), np.array(io), np.array(sy)
 
 
-def test_fixed_length_code_resynchronises_within_km_regions(emu):
-    """5-bit fixed-length code: region starts 288*j hit a code boundary every
-    5 regions, so walks cross up to 4 covered regions and still merge."""
+def test_fixed_length_code_on_the_lattice(emu):
+    """5-bit fixed-length code: the default region size is a multiple of 5
+    (160 bits), so every region starts on a code boundary and every walk
+    merges at once."""
     iz, io, sy = complete_tree(5)
     rng = np.random.default_rng(1)
     bits = 5 * 40000
     data = rng.integers(0, 256, size=bits // 8 + 1).astype(np.uint8)
     ref = oracle_chain(iz, io, sy, data, bits)
-    n, out, st = run_emu(emu, iz, io, sy, data, bits, 288)
+    n, out, st = run_emu(emu, iz, io, sy, data, bits, 0)
+    assert st[3] % 5 == 0 and st[3] % 32 == 0
     assert n == len(ref) == 40000 and np.array_equal(out, ref)
-    assert st[3] == 5
+    assert st[1] == 0
+
+
+def test_fixed_length_code_off_the_lattice_multi_region_walks(emu):
+    """The same 5-bit code with 256-bit regions: region starts drift by one
+    bit per region against the code lattice, so walks cross up to 5 regions
+    before they merge (covered regions, k > 1) -- and the tiles' leaving
+    state is the entering one shifted, exercising the transfer tables."""
+    iz, io, sy = complete_tree(5)
+    rng = np.random.default_rng(3)
+    bits = 5 * 100000
+    data = rng.integers(0, 256, size=bits // 8 + 1).astype(np.uint8)
+    ref = oracle_chain(iz, io, sy, data, bits)
+    n, out, st = run_emu(emu, iz, io, sy, data, bits, 256)
+    assert n == len(ref) == 100000 and np.array_equal(out, ref)
+    assert st[4] == 5 and st[1] > 0
 
 
 def test_non_synchronising_code_is_detected(emu):
-    """An 11-bit fixed-length code needs up to 11 regions to realign with
-    288-bit regions (> HH_KM): the walks must fail (-> exact path), never
-    mis-decode; a region size that is a multiple of 11 aligns at once."""
+    """An 11-bit fixed-length code realigns with 96-bit regions only every
+    11 regions (> HH_KM): the walks must fail (-> exact path), never
+    mis-decode; the default region size (352 = lcm(32, 11)) aligns at once."""
     iz, io, sy = complete_tree(11)
     rng = np.random.default_rng(2)
     bits = 11 * 30000
     data = rng.integers(0, 256, size=bits // 8 + 1).astype(np.uint8)
     ref = oracle_chain(iz, io, sy, data, bits)
-    n, out, st = run_emu(emu, iz, io, sy, data, bits, 288)
+    n, out, st = run_emu(emu, iz, io, sy, data, bits, 96)
     assert n == UNSUPPORTED and st[2] > 0
-    n, out, st = run_emu(emu, iz, io, sy, data, bits, 286)
-    assert n == len(ref) and np.array_equal(out, ref) and st[3] == 1
+    n, out, st = run_emu(emu, iz, io, sy, data, bits, 0)
+    assert st[3] == 352
+    assert n == len(ref) and np.array_equal(out, ref)

@@ -66,3 +66,127 @@ def test_stage_pipeline(hh, dec, files_dir, name):
     torch.cuda.synchronize()
     assert n == len(ref)
     assert np.array_equal(d_out[:n].cpu().numpy(), ref)
+
+
+def _random_tree(rng, nleaves):
+    izero, ione, sym = [-1], [-1], [0]
+    leaves = [0]
+    syms = rng.permutation(256)[:nleaves]
+    while len(leaves) < nleaves:
+        v = leaves.pop(int(rng.integers(len(leaves))))
+        a, b = len(izero), len(izero) + 1
+        izero[v], ione[v] = a, b
+        sym[v] = int(rng.integers(256))
+        izero += [-1, -1]; ione += [-1, -1]; sym += [0, 0]
+        leaves += [a, b]
+    for k, v in enumerate(leaves):
+        sym[v] = int(syms[k])
+    return np.array(izero), np.array(ione), np.array(sym), syms
+
+
+def _complete_tree(depth):
+    iz, io, sy = [-1], [-1], [0]
+    frontier = [0]
+    for _ in range(depth):
+        nxt = []
+        for v in frontier:
+            a, b = len(iz), len(iz) + 1
+            iz[v], io[v] = a, b
+            iz += [-1, -1]; io += [-1, -1]; sy += [0, 0]
+            nxt += [a, b]
+        frontier = nxt
+    for k, v in enumerate(frontier):
+        sy[v] = k & 255
+    return np.array(iz), np.array(io), np.array(sy)
+
+
+def _oracle(iz, io, sy, data, bits):
+    hf = O.Huff(bits, 0, np.asarray(iz, np.int32), np.asarray(io, np.int32),
+                np.asarray(sy, np.uint8), np.asarray(data, np.uint8)[: (bits + 7) // 8])
+    return O.OracleHuff.from_arrays(hf).chain_decode()
+
+
+def _decode_dev(hh, dec, data, bits, cap):
+    import torch
+    buf = np.zeros((bits + 7) // 8 + 64, np.uint8)
+    buf[: (bits + 7) // 8] = np.asarray(data, np.uint8)[: (bits + 7) // 8]
+    d_in = torch.from_numpy(buf).cuda()
+    d_out = torch.zeros(cap + 64, dtype=torch.uint8, device="cuda")
+    n = dec.decode_device(d_in, bits, d_out)
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    assert int(out[n:].astype(np.int64).sum()) == 0, "bytes written past the output"
+    return out[:n]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_trees_and_cut_streams(hh, seed):
+    """Random codes and streams (multi-tile), cut at arbitrary bits: the
+    reference's tail rule for a code cut off by the end of the stream."""
+    rng = np.random.default_rng(100 + seed)
+    nleaves = int(rng.integers(2, 150))
+    iz, io, sy, syms = _random_tree(rng, nleaves)
+    t = hh.Tree(iz, io, sy)
+    if t.info()["maxlen"] > 60:
+        pytest.skip("encoder limit")
+    p = rng.dirichlet(np.full(nleaves, 0.3))
+    text = rng.choice(syms, size=int(rng.integers(200000, 900000)), p=p).astype(np.uint8)
+    data, bits = t.encode(text)
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(t)
+        for cut in (bits, bits - 1, bits // 3 + 7):
+            ref = _oracle(iz, io, sy, data, cut)
+            got = _decode_dev(hh, dec, data, cut, cut + 16)
+            assert len(got) == len(ref) and np.array_equal(got, ref), cut
+            assert dec.stats()["exact_fallback"] == 0
+    finally:
+        dec.close()
+
+
+def test_multi_region_walks_and_transfer_tables(hh):
+    """5-bit fixed-length code with 256-bit regions: region starts drift one
+    bit per region against the code lattice, so walks cover up to 4 regions
+    and tiles leave non-CONST states (look-back through the tables)."""
+    iz, io, sy = _complete_tree(5)
+    rng = np.random.default_rng(7)
+    bits = 5 * 600000
+    data = rng.integers(0, 256, size=bits // 8 + 1).astype(np.uint8)
+    ref = _oracle(iz, io, sy, data, bits)
+    dec = hh.Decoder(0, lane_bits=256)
+    try:
+        dec.set_tree(hh.Tree(iz, io, sy))
+        got = _decode_dev(hh, dec, data, bits, bits)
+        assert dec.stats()["exact_fallback"] == 0
+        assert len(got) == len(ref) and np.array_equal(got, ref)
+    finally:
+        dec.close()
+
+
+def test_output_window_rounds(hh, files_dir, monkeypatch):
+    """A 4 KiB LDS output window forces several emission rounds per tile."""
+    monkeypatch.setenv("HH_OB_KIB", "4")
+    for name in ("E.coli", "kjv.txt"):
+        path = os.path.join(files_dir, name + ".huff")
+        hf = hh.HuffFile.load(path)
+        ref = O.OracleHuff.load(path).chain_decode()
+        dec = hh.Decoder(0)
+        try:
+            dec.set_tree(hf.tree())
+            got = _decode_dev(hh, dec, hf.payload, hf.bits, hf.uncompressedsize)
+            assert dec.stats()["exact_fallback"] == 0
+            assert np.array_equal(got, ref)
+        finally:
+            dec.close()
+
+
+def test_capacity_error(hh, files_dir):
+    path = os.path.join(files_dir, "paper1.huff")
+    hf = hh.HuffFile.load(path)
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(hf.tree())
+        with pytest.raises(hh.HipHuffError):
+            dec.decode_host(hf.payload, hf.bits, hf.uncompressedsize - 1)
+    finally:
+        dec.close()
