@@ -61,11 +61,11 @@
 /*   (HH_NLS is a multiple of 32) however far apart the lanes' chains    */
 /*   are.                                                                */
 /* ------------------------------------------------------------------ */
-#define HH_NL 512
+#define HH_NL 256
 #define HH_NR HH_NL           /* regions per tile */
 #define HH_KM 8               /* max regions one walk may cross */
 #define HH_NCOL (HH_NR + HH_KM + 1)   /* staged columns */
-#define HH_NLS 544            /* >= HH_NCOL, multiple of 32 */
+#define HH_NLS 288            /* >= HH_NCOL, multiple of 32 */
 #define HH_SW_MAX 12          /* max words per region (S <= 384) */
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
                                  as a failed walk) */
@@ -96,21 +96,36 @@ typedef struct {
     const uint32_t *tree; /* compact tree (tail symbols, very long codes) */
     const uint8_t *tsym;
     uint32_t bt;          /* end of stream relative to the tile (clamped) */
+    uint32_t maxadv;      /* most bits one table step advances:
+                             max(HH_P, longest code), <= 32             */
 } hh_ctx;
 
 /* The kernel is instantiated per words-per-region (the kernel's hh_ctx has
  * a compile-time sw), so this division folds to shifts / a multiply-high. */
-HH_HD uint32_t hh_word(const hh_ctx *c, uint32_t g) {
-    uint32_t r = g / c->sw;
-    uint32_t k = g - r * c->sw;
-    return c->w[k * HH_NLS + r];
+HH_HD uint32_t hh_idx(const hh_ctx *c, uint32_t g) {
+    const uint32_t r = g / c->sw;
+    return (g - r * c->sw) * HH_NLS + r;
+}
+/* LDS index of the word after the one at index a */
+HH_HD uint32_t hh_idx_next(const hh_ctx *c, uint32_t a) {
+    const uint32_t last = (c->sw - 1) * HH_NLS;
+    return a >= last ? a - last + 1 : a + HH_NLS;
+}
+HH_HD uint32_t hh_word(const hh_ctx *c, uint32_t g) { return c->w[hh_idx(c, g)]; }
+
+HH_HD uint32_t hh_funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (sh & 31));
+#endif
 }
 
 /* 32 stream bits from tile position p, stream bit p in bit 0 (LSB-first
  * bytes: the reference's window convention, linapproach.c:207-209). */
 HH_HD uint32_t hh_win(const hh_ctx *c, uint32_t p) {
-    uint32_t g = p >> 5;
-    uint32_t lo = hh_word(c, g), hi = hh_word(c, g + 1);
+    const uint32_t a = hh_idx(c, p >> 5);
+    uint32_t lo = c->w[a], hi = c->w[hh_idx_next(c, a)];
 #if defined(__HIP_DEVICE_COMPILE__)
     return __builtin_amdgcn_alignbit(hi, lo, p & 31);
 #else
@@ -165,8 +180,7 @@ typedef struct {
     uint32_t nb, ns, bm, len0, syms;
 } hh_look;
 
-HH_HD hh_look hh_lookup(const hh_ctx *c, uint32_t p) {
-    uint32_t win = hh_win(c, p);
+HH_HD hh_look hh_lookup_w(const hh_ctx *c, uint32_t p, uint32_t win) {
     uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
     hh_look L;
     L.ns = HH_L1_NSYM(e);
@@ -185,6 +199,40 @@ HH_HD hh_look hh_lookup(const hh_ctx *c, uint32_t p) {
     return L;
 }
 
+HH_HD hh_look hh_lookup(const hh_ctx *c, uint32_t p) { return hh_lookup_w(c, p, hh_win(c, p)); }
+
+/* ------------------------------------------------------------------ */
+/* Chain cursor: position p with words p>>5 and p>>5 + 1 in registers and */
+/* word p>>5 + 2 preloaded, so a decode step does its table lookup with no */
+/* dependent LDS read in front of it.  A step advances <= 32 bits (codes   */
+/* of the fast path are <= 32 bits), i.e. crosses at most one word.        */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint32_t p, lo, hi, nx, a;   /* a: LDS index of word p>>5 + 2 (held in nx) */
+} hh_cur;
+
+HH_HD hh_cur hh_cur_at(const hh_ctx *c, uint32_t p) {
+    hh_cur u;
+    const uint32_t a0 = hh_idx(c, p >> 5), a1 = hh_idx_next(c, a0);
+    u.p = p;
+    u.lo = c->w[a0];
+    u.hi = c->w[a1];
+    u.a = hh_idx_next(c, a1);
+    u.nx = c->w[u.a];
+    return u;
+}
+HH_HD uint32_t hh_cur_win(const hh_cur &u) { return hh_funnel(u.hi, u.lo, u.p & 31); }
+HH_HD void hh_cur_adv(const hh_ctx *c, hh_cur &u, uint32_t adv) {
+    const uint32_t np = u.p + adv;
+    const bool cross = (np >> 5) != (u.p >> 5);
+    u.p = np;
+    u.lo = cross ? u.hi : u.lo;
+    u.hi = cross ? u.nx : u.hi;
+    const uint32_t an = hh_idx_next(c, u.a);
+    u.a = cross ? an : u.a;
+    u.nx = c->w[u.a];
+}
+
 /* Offset of the lookup's first boundary at or after offset d (>= 1): a
  * symbol start inside the lookup, or nb (the next lookup's start). */
 HH_HD uint32_t hh_first_ge(const hh_look &L, uint32_t d) {
@@ -197,66 +245,167 @@ HH_HD uint32_t hh_syms_before(const hh_look &L, uint32_t o) { return hh_popc(L.b
 /* Pass 1 (decodeallbits restated): the chain from p0 (< lim), counting the
  * symbols that start in [p0, lim) (lim <= bt).  Returns the exit: the
  * chain's first position >= lim (bt if the stream ends first). */
-HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint32_t *count) {
-    uint32_t p = p0, n = 0;
-    while (p < lim) {
-        hh_look L = hh_lookup(c, p);
-        uint32_t o = hh_first_ge(L, lim - p);
-        n += hh_syms_before(L, o);
-        p += o;
+HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint32_t *count,
+                               uint32_t *mask = nullptr) {
+    hh_cur u = hh_cur_at(c, p0);
+    uint32_t n = 0;
+    /* boundary mask of the chain (bit i of tile word g <=> a symbol starts
+     * at 32 g + i), stored in the same transposed layout as the words; the
+     * region starts word-aligned.  (mlo, mhi) accumulate the words p>>5 and
+     * p>>5 + 1; am is the LDS index of word p>>5. */
+    uint32_t mlo = 0, mhi = 0, am = hh_idx(c, p0 >> 5);
+    /* main loop: every symbol of a step starts before lim */
+    const uint32_t lf = lim > c->maxadv ? lim - c->maxadv : 0u;
+    while (u.p < lf) {
+        const uint32_t win = hh_cur_win(u);
+        const uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
+        uint32_t ns = HH_L1_NSYM(e), nb = HH_L1_NBITS(e), bm = HH_L1_BMASK(e);
+        if (ns == 0) {
+            uint32_t s;
+            nb = hh_escape(c, u.p, win, e, &s);
+            ns = 1;
+            bm = 1;
+        }
+        n += ns;
+        if (mask) {
+            const uint64_t m = (uint64_t)bm << (u.p & 31);
+            mlo |= (uint32_t)m;
+            mhi |= (uint32_t)(m >> 32);
+            mask[am] = mlo;
+            const bool cross = ((u.p + nb) >> 5) != (u.p >> 5);
+            mlo = cross ? mhi : mlo;
+            mhi = cross ? 0u : mhi;
+            am = cross ? hh_idx_next(c, am) : am;
+        }
+        hh_cur_adv(c, u, nb);
     }
+    /* tail: count only the symbols that start before lim */
+    while (u.p < lim) {
+        hh_look L = hh_lookup_w(c, u.p, hh_cur_win(u));
+        const uint32_t o = hh_first_ge(L, lim - u.p);
+        n += hh_syms_before(L, o);
+        if (mask) {
+            const uint64_t m = (uint64_t)(L.bm & hh_lowmask(o)) << (u.p & 31);
+            mlo |= (uint32_t)m;
+            mhi |= (uint32_t)(m >> 32);
+            mask[am] = mlo;
+            const bool cross = ((u.p + o) >> 5) != (u.p >> 5);
+            mlo = cross ? mhi : mlo;
+            mhi = cross ? 0u : mhi;
+            am = cross ? hh_idx_next(c, am) : am;
+        }
+        hh_cur_adv(c, u, o);
+    }
+    /* the word the chain stopped in, if it is still inside the region */
+    if (mask && (u.p >> 5) < (p0 >> 5) + c->sw) mask[am] = mlo;
     *count = n;
-    return p < c->bt ? p : c->bt;
+    return u.p < c->bt ? u.p : c->bt;
 }
 
-/* Pass 2 (makebigtable restated): the chain W leaving region j at x (its
- * exit) walked against the offset-0 chain C of region j+1, two pointers: the
- * one behind moves to its first boundary at or past min(other, region end).
- * Equal positions = merged.  Both at/past the region end without meeting =
- * region j+1 is COVERED by W; W (now at its first boundary past that
- * region's start) carries on against region j+2's chain, and so on, up to
- * HH_KM regions.  Any common boundary is a valid merge point: after it the
- * chains are identical, so counts taken there are exact.
+/* Symbols of a region's own chain that start before region offset off
+ * (popcount of its mask below off). */
+HH_HD uint32_t hh_mask_rank(const hh_ctx *c, const uint32_t *mask, uint32_t R, uint32_t off) {
+    uint32_t cnt = 0, a = hh_idx(c, R >> 5);
+    for (uint32_t w = 0; w < (off >> 5); w++) {
+        cnt += hh_popc(mask[a]);
+        a = hh_idx_next(c, a);
+    }
+    return cnt + hh_popc(mask[a] & hh_lowmask(off & 31));
+}
+
+/* Pass 2 (makebigtable restated).  The chain W leaving region j at its
+ * exit x is followed region by region.  In region r (r = j+1, ...) W is
+ * tested against r's own offset-0 chain C_r:
+ *   - with C_r's boundary mask (regions of this tile): each table step of W
+ *     tests its symbol starts against the mask -- the first common start is
+ *     the merge;
+ *   - without a mask (regions of the next tile): two pointers, the one
+ *     behind moves to its first boundary at or past min(other, region end).
+ * W reaching its first boundary at or past the region end equal to C_r's
+ * exit x_r is a merge there too.  Otherwise region r is COVERED by W, which
+ * carries on into region r+1 (up to HH_KM regions).  Any common boundary is
+ * a valid merge point: after it the chains are identical, so counts taken
+ * there are exact.
  *   k     regions crossed (1 = merged in region j+1), 0 = no merge
  *   e     W's first boundary in the merge region, as an offset from its start
  *   cov   W's symbols from x up to that boundary (the covered regions)
- *   delta W's symbols from there to the merge minus C's symbols before it */
+ *   delta W's symbols from there to the merge minus C's symbols before it
+ * mask/xs/ns (may be null): masks, exits and counts of regions < nmask. */
 typedef struct {
     uint32_t k, e, cov;
     int32_t delta;
 } hh_wk;
 
-HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x) {
+HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
+                    const uint32_t *mask = nullptr, const uint32_t *xs = nullptr,
+                    const uint16_t *ns = nullptr, uint32_t nmask = 0) {
     hh_wk r = {0u, 0u, 0u, 0};
     const uint32_t bt = c->bt;
     uint32_t A = x < bt ? x : bt;
     int32_t ca = 0;
     uint32_t it = 0;
     for (uint32_t k = 1; k <= HH_KM; k++) {
-        const uint32_t R = (j + k) * S;
+        const uint32_t rg = j + k;
+        const uint32_t R = rg * S;
         const uint32_t Ec = R + S < bt ? R + S : bt;
         const int32_t ca0 = ca;
         const uint32_t e = A > R ? A - R : 0u;   /* A == bt <= R: stream ended */
-        uint32_t B = R < bt ? R : bt;
-        int32_t cb = 0;
-        for (; it < HH_WALK_MAX; it++) {
-            if (A == B) {
+        if (mask && rg < nmask) {
+            for (; A < Ec && it < HH_WALK_MAX; it++) {
+                hh_look L = hh_lookup(c, A);
+                const uint32_t off = A - R;
+                const uint32_t a0 = hh_idx(c, (R >> 5) + (off >> 5));
+                const uint32_t m = hh_funnel(mask[hh_idx_next(c, a0)], mask[a0], off & 31);
+                const uint32_t hit = L.bm & m & hh_lowmask(Ec - A);
+                if (hit) {
+                    const uint32_t t = hh_ctz(hit);
+                    ca += (int32_t)hh_popc(L.bm & hh_lowmask(t));
+                    r.k = k;
+                    r.e = e;
+                    r.cov = (uint32_t)ca0;
+                    r.delta = (ca - ca0) - (int32_t)hh_mask_rank(c, mask, R, off + t);
+                    return r;
+                }
+                if (A + L.nb <= Ec) {
+                    A += L.nb;
+                    ca += (int32_t)L.ns;
+                } else {
+                    const uint32_t o = hh_first_ge(L, Ec - A);
+                    ca += (int32_t)hh_syms_before(L, o);
+                    A += o;
+                }
+            }
+            if (A > bt) A = bt;
+            const uint32_t xr = xs[rg] < bt ? xs[rg] : bt;
+            if (A == xr) {                  /* merged at the region's exit */
                 r.k = k;
                 r.e = e;
                 r.cov = (uint32_t)ca0;
-                r.delta = (ca - ca0) - cb;
+                r.delta = (ca - ca0) - (int32_t)ns[rg];
                 return r;
             }
-            const bool mvA = A < B;
-            const uint32_t P = mvA ? A : B, Q = mvA ? B : A;
-            if (P >= Ec) break;                  /* both past the region end */
-            const uint32_t tgt = Q < Ec ? Q : Ec;
-            hh_look L = hh_lookup(c, P);
-            const uint32_t o = hh_first_ge(L, tgt - P);
-            const int32_t n = (int32_t)hh_syms_before(L, o);
-            uint32_t np = P + o;
-            if (np > bt) np = bt;
-            if (mvA) { A = np; ca += n; } else { B = np; cb += n; }
+        } else {
+            uint32_t B = R < bt ? R : bt;
+            int32_t cb = 0;
+            for (; it < HH_WALK_MAX; it++) {
+                if (A == B) {
+                    r.k = k;
+                    r.e = e;
+                    r.cov = (uint32_t)ca0;
+                    r.delta = (ca - ca0) - cb;
+                    return r;
+                }
+                const bool mvA = A < B;
+                const uint32_t P = mvA ? A : B, Q = mvA ? B : A;
+                if (P >= Ec) break;              /* both past the region end */
+                const uint32_t tgt = Q < Ec ? Q : Ec;
+                hh_look L = hh_lookup(c, P);
+                const uint32_t o = hh_first_ge(L, tgt - P);
+                const int32_t n = (int32_t)hh_syms_before(L, o);
+                uint32_t np = P + o;
+                if (np > bt) np = bt;
+                if (mvA) { A = np; ca += n; } else { B = np; cb += n; }
+            }
         }
         if (it >= HH_WALK_MAX) break;
     }
@@ -299,21 +448,26 @@ HH_HD uint32_t hh_mem_init(uint32_t j) { return j < HH_KM - 1 ? (2u << j) - 1u :
  * ends at whi.  Takes a whole lookup when it fits both, else one symbol
  * (with the tail rule at bt).  Returns the symbols taken (k) in *val (first
  * in bits 0..7) and the bits advanced. */
-HH_HD uint32_t hh_emit_step(const hh_ctx *c, uint32_t p, uint32_t pe, uint64_t o, uint64_t whi,
+HH_HD uint32_t hh_emit_step(const hh_ctx *c, hh_cur &u, uint32_t pe, uint64_t o, uint64_t whi,
                             uint32_t *val, uint32_t *k) {
-    hh_look L = hh_lookup(c, p);
+    const uint32_t p = u.p;
+    hh_look L = hh_lookup_w(c, p, hh_cur_win(u));
+    uint32_t adv;
     if (p + L.nb <= pe && o + L.ns <= whi) {
         *val = L.syms;
         *k = L.ns;
-        return L.nb;
+        adv = L.nb;
+    } else {
+        adv = L.len0;
+        uint32_t s = L.syms & 0xffu;
+        if (adv > c->bt - p) {
+            s = hh_tail_symbol(c, p);
+            adv = c->bt - p;
+        }
+        *val = s;
+        *k = 1;
     }
-    uint32_t adv = L.len0, s = L.syms & 0xffu;
-    if (adv > c->bt - p) {
-        s = hh_tail_symbol(c, p);
-        adv = c->bt - p;
-    }
-    *val = s;
-    *k = 1;
+    hh_cur_adv(c, u, adv);
     return adv;
 }
 

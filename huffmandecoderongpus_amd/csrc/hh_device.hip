@@ -32,8 +32,8 @@
 #include "hh_internal.h"
 #include "hiphuff.h"
 
-#define HH_OB_DEFAULT (32u << 10)   // LDS output window per workgroup (bytes)
-#define HH_MAXLEN_FAST 64           // longest code the fast path stages for
+#define HH_OB_DEFAULT (16u << 10)   // LDS output window per workgroup (bytes)
+#define HH_MAXLEN_FAST 32           // longest code of the fast path (one cursor step <= 32 bits)
 
 #define HIP_OK(x)                                                             \
     do {                                                                      \
@@ -59,8 +59,9 @@ enum { F_FAIL = 1, F_OVER = 2, F_TIMEOUT = 8 };
 #define HH_SPIN_LIMIT (1u << 22)
 
 struct LookBack {
-    uint64_t *agg;       // [ntiles] aggregate granules (table entry d = 0 + CONST)
+    uint64_t *agg;       // [ntiles] aggregate granules (table row d = 0 + CONST)
     uint64_t *inc;       // [ntiles] inclusive granules (prefix + resolved state)
+    uint64_t *tabs;      // [ntiles][HH_KM] table rows d >= 1 as granules
     uint64_t *tdbg;      // diagnostic (HH_DEBUG_TILES): [ntiles][8] base, size|state, excl, table entry,
                          //   look-back: inclusive tile, its prefix, counts summed, rounds
 };
@@ -156,12 +157,13 @@ __device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t *fla
     return hh_inc_state(poll_granule(&lb.inc[t - 1], flags));
 }
 
-// Exclusive charged prefix of tile t (t >= 1), one wave: 64 predecessors per
-// round, the nearest inclusive granule ends the look-back.  A tile's
-// aggregate is its count for entering d = 0; the state entering tile u comes
-// from the inclusive of u-1 if that is the nearest one, else from u-1's
-// aggregate, which must be CONST.  Otherwise (or if u is entered with d > 0)
-// the look-back waits until an inclusive granule appears closer.
+// Exclusive charged prefix of tile t (t >= 1), one wave, 64 x HH_LBV
+// predecessors per round; the nearest inclusive granule ends the look-back.
+// Tile u counts with its table row for the state entering it: that state
+// comes from the inclusive of u-1 if that is the nearest one, else from
+// u-1's aggregate, which must be CONST (otherwise wait until an inclusive
+// granule appears closer); row 0 is u's aggregate, rows d > 0 are granules
+// of their own.
 #define HH_LBV 8   // tiles per lane per look-back round (512-tile window)
 __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flags) {
     constexpr uint32_t V = HH_LBV;
@@ -177,6 +179,7 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flag
         uint64_t iv[V], av[V + 1];
         uint32_t ofirst, spins = 0, lf;
         uint64_t incv;
+        int64_t csum = 0;
         for (;;) {
 #pragma unroll
             for (uint32_t i = 0; i <= V; i++) {
@@ -198,6 +201,7 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flag
             for (uint32_t i = 0; i < V; i++) if (i == lf) myinc = iv[i];
             incv = shfl64(myinc, (int)(fl & 63u));
             bool ok = true;
+            csum = 0;
 #pragma unroll
             for (uint32_t i = 0; i < V; i++) {
                 const uint32_t o = lane * V + i;
@@ -205,10 +209,12 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flag
                     const bool pin = o + 1 == ofirst;
                     const uint64_t pv = av[i + 1];
                     const bool known = pin || ((pv >> HH_ST_SHIFT) != 0 && (pv & HH_CST));
-                    const uint32_t st = pin ? hh_inc_state(incv) : hh_tab_state(pv);
-                    // entered with d > 0: row d = 0 does not apply, wait for the
-                    // tile's own inclusive prefix
-                    ok = ok && (av[i] >> HH_ST_SHIFT) != 0 && known && hh_state_d(st) == 0;
+                    const uint32_t d = hh_state_d(pin ? hh_inc_state(incv) : hh_tab_state(pv));
+                    // entered with d > 0: that row of the tile's table (a granule)
+                    uint64_t row = av[i];
+                    if (known && d != 0) row = ld_sc1(&lb.tabs[(uint64_t)(ub - (int64_t)i) * HH_KM + d]);
+                    ok = ok && (av[i] >> HH_ST_SHIFT) != 0 && known && (row >> HH_ST_SHIFT) != 0;
+                    csum += hh_tab_count(row);
                 }
             }
             if (!__ballot(!ok)) break;
@@ -218,11 +224,7 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flag
                 return 0;
             }
         }
-        int64_t c = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < V; i++)
-            if (lane * V + i < ofirst) c += hh_tab_count(av[i]);
-        excl += wave_sum64((uint64_t)c);
+        excl += wave_sum64((uint64_t)csum);
         rounds++;
         if (ofirst < 64u * V) {
             const uint64_t pre = incv & HH_INC_MASK;
@@ -320,243 +322,285 @@ struct Geometry {
     uint32_t S, sw, magic;
     uint32_t ob;         // LDS output window bytes (multiple of 16)
     uint32_t vec4;       // 16-B aligned payload and sw % 4 == 0
+    uint32_t maxadv;     // max(HH_P, longest code)
+};
+
+// Per-lane results of a tile's front half, kept in registers until its back
+// half (one iteration later).
+struct LaneRec {
+    uint32_t n;          // own-chain symbols in the region (pass 1)
+    uint32_t k, e, cov;  // walk: regions crossed, entry offset, covered symbols
+    int32_t delta;       // walk correction
 };
 
 template <uint32_t SW>
-__global__ __launch_bounds__(HH_NL, 4) void k_decode(const uint32_t *__restrict__ gdata, Geometry geo,
-                                                  DevTab tab, LookBack lb,
-                                                  uint8_t *__restrict__ out, uint64_t cap,
-                                                  uint32_t *flags, uint64_t *dbg) {
+__global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict__ gdata, Geometry geo,
+                                                     DevTab tab, LookBack lb,
+                                                     uint8_t *__restrict__ out, uint64_t cap,
+                                                     uint32_t *flags, uint64_t *dbg) {
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ uint32_t s_ein[HH_NL];          // run entries pushed by walkers
     __shared__ int16_t s_din[HH_NL];           // their deltas
     __shared__ uint16_t s_exc[HH_NL];          // exception lanes (k > 1)
-    __shared__ uint8_t s_mem[HH_NL];           // live masks over entering d
+    __shared__ uint8_t s_mem[2][HH_NL];        // live masks over entering d (per pending tile)
     __shared__ uint8_t s_k[HH_NL];
     __shared__ int32_t s_part[HH_NL / 64][HH_KM];
     __shared__ uint32_t s_ost[HH_KM];
-    __shared__ uint64_t s_tab[HH_KM];
+    __shared__ uint64_t s_tab[2][HH_KM];       // transfer table (per pending tile)
     __shared__ int32_t s_tmp[HH_NL / 64];
     __shared__ uint32_t s_cnt[HH_NL / 64];
     __shared__ uint64_t s_bc[4];
+    __shared__ uint32_t s_x[HH_NR];            // pass-1 exits and counts of the front tile
+    __shared__ uint16_t s_n[HH_NR];
 
+    constexpr uint32_t S = 32 * SW;
     uint64_t *s_l1 = (uint64_t *)smem;
-    uint32_t *s_w = (uint32_t *)(smem + HH_L1_SIZE * 8);
-    uint8_t *s_out = (uint8_t *)(s_w + SW * HH_NLS);
+    uint32_t *s_wb = (uint32_t *)(smem + HH_L1_SIZE * 8);       // 2 x SW * HH_NLS words
+    uint32_t *s_mk = s_wb + 2 * SW * HH_NLS;                     // SW * HH_NLS boundary-mask words
+    uint8_t *s_out = (uint8_t *)(s_mk + SW * HH_NLS);
     uint32_t *s_l2 = (uint32_t *)(s_out + geo.ob + 16);
 
     const uint32_t j = threadIdx.x;
-    constexpr uint32_t S = 32 * SW;
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
     const uint32_t span = HH_NCOL * S;          // bits staged per tile
+    const uint64_t G = gridDim.x;
     STAMP_DECL
 
     for (uint32_t i = j; i < HH_L1_SIZE; i += HH_NL) s_l1[i] = tab.l1[i];
     for (uint32_t i = j; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
 
-    uint64_t t = blockIdx.x;
-    Prefetch pf;
-    if (t < geo.ntiles) prefetch_tile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords, geo.vec4);
-
     hh_ctx c;
-    c.w = s_w;
     c.sw = SW;
     c.magic = 0;
     c.l1 = s_l1;
     c.l2 = s_l2;
     c.tree = tab.tree;
     c.tsym = tab.tsym;
+    c.maxadv = geo.maxadv;
 
-    for (; t < geo.ntiles; t += gridDim.x) {
-        const uint64_t T0 = t * tile_bits;
-        const uint64_t rem = geo.bits - T0;
-        const uint32_t bt = rem < span ? (uint32_t)rem : span;
-        c.bt = bt;
-        __syncthreads();                 // previous tile done with s_w
-        store_tile<SW>(pf, s_w);
-        const uint64_t tn = t + gridDim.x;
-        if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
-        __syncthreads();
-        STAMP(0);
+    Prefetch pf;
+    uint64_t tn = blockIdx.x;                   // tile for the next front half
+    if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
 
-        // pass 1: own region from offset 0
-        const uint32_t p0 = j * S;
-        uint32_t n = 0, x = bt;
-        if (p0 < bt) {
-            const uint32_t lim = p0 + S < bt ? p0 + S : bt;
-            x = hh_region_count(&c, p0, lim, &n);
-        }
-        STAMP(1);
+    LaneRec rp = {0u, 1u, 0u, 0u, 0};           // the pending tile (front done)
+    uint64_t tp = ~0ull;
+    uint32_t par = 0;                           // buffer parity of the next front half
 
-        // walks: region j's exit against the next regions' own chains
-        const hh_wk wk = hh_walk(&c, j, S, x);
-        if (wk.k == 0) {
-            // first failure: tile, lane, exit, count (hh_debug_failure)
-            atomicOr(flags, (uint32_t)F_FAIL);
-            if (atomicCAS(&flags[4], 0u, 1u) == 0u) {
-                flags[5] = (uint32_t)t; flags[6] = j; flags[7] = x; flags[8] = n; flags[9] = bt;
+    for (;;) {
+        const bool front = tn < geo.ntiles, back = tp < geo.ntiles;
+        if (!front && !back) break;
+        LaneRec rn = rp;
+        __syncthreads();                        // buffer `par` no longer read by a back half
+        if (front) {
+            // ---------------- front half of tile tn ----------------
+            uint32_t *s_w = s_wb + par * SW * HH_NLS;
+            c.w = s_w;
+            const uint64_t rem = geo.bits - tn * tile_bits;
+            c.bt = rem < span ? (uint32_t)rem : span;
+            const uint32_t bt = c.bt;
+            store_tile<SW>(pf, s_w);
+            if (tn + G < geo.ntiles) prefetch_tile<SW>(pf, gdata, (tn + G) * tile_bits / 32, geo.nwords, geo.vec4);
+            __syncthreads();
+            STAMP(0);
+
+            // pass 1: own region from offset 0
+            const uint32_t p0 = j * S;
+            uint32_t n = 0, x = bt;
+            if (p0 < bt) {
+                const uint32_t lim = p0 + S < bt ? p0 + S : bt;
+                x = hh_region_count(&c, p0, lim, &n, s_mk);
             }
-        }
-        const uint32_t kk = wk.k ? wk.k : 1u;
-        s_k[j] = (uint8_t)kk;
-        s_mem[j] = (uint8_t)hh_mem_init(j);
-        STAMP(2);
+            s_x[j] = x;
+            s_n[j] = (uint16_t)n;
+            __syncthreads();
+            STAMP(1);
 
-        // transfer table: live masks (exceptions, ascending, by one lane),
-        // charged count and leaving state for every entering d
-        const uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt);   // barriers inside
-        if (j == 0) {
-            for (uint32_t i = 0; i < nexc; i++) {
-                const uint32_t e = s_exc[i], ke = s_k[e];
-                const uint8_t m = s_mem[e];
-                for (uint32_t q = e + 1; q < e + ke && q < HH_NR; q++) s_mem[q] &= (uint8_t)~m;
+            // walks: region j's exit against the next regions' own chains
+            const hh_wk wk = hh_walk(&c, j, S, x, s_mk, s_x, s_n, HH_NR);
+            if (wk.k == 0) {
+                atomicOr(flags, (uint32_t)F_FAIL);
+                if (atomicCAS(&flags[4], 0u, 1u) == 0u) {
+                    flags[5] = (uint32_t)tn; flags[6] = j; flags[7] = x; flags[8] = n; flags[9] = bt;
+                }
             }
-        }
-        __syncthreads();
-        const uint32_t mem = s_mem[j];
-        const int32_t charged = (int32_t)(n + wk.cov) + wk.delta;
-        if (j + kk >= HH_NR) {
-            const uint32_t os = hh_state_pack(j + kk - HH_NR, wk.e, wk.delta);
-#pragma unroll
-            for (uint32_t d = 0; d < HH_KM; d++)
-                if ((mem >> d) & 1u) s_ost[d] = os;
-        }
-#pragma unroll
-        for (uint32_t d = 0; d < HH_KM; d++) {
-            const int32_t v = wave_sum(((mem >> d) & 1u) ? charged : 0);
-            if ((j & 63u) == 0) s_part[j >> 6][d] = v;
-        }
-        __syncthreads();
-        if (j < HH_KM) {
-            int32_t cnt = 0;
-#pragma unroll
-            for (uint32_t w = 0; w < HH_NL / 64; w++) cnt += s_part[w][j];
-            s_tab[j] = hh_tab_pack(cnt, s_ost[j]);
-        }
-        __syncthreads();
-        if (j == 0) {
-            // aggregate = table row d = 0; rows d >= 1 stay in LDS (a tile entered
-            // with d >= 1 publishes its inclusive prefix, look-backs wait for it)
-            bool cst = true;
-            for (uint32_t d = 1; d < HH_KM; d++) cst = cst && hh_tab_state(s_tab[d]) == hh_tab_state(s_tab[0]);
-            st_sc1(&lb.agg[t], HH_AGG | (cst ? HH_CST : 0ull) | s_tab[0]);
-            // state entering this tile
-            s_bc[0] = entering_state(lb, t, flags);
-        }
-        __syncthreads();
-        STAMP(3);
+            const uint32_t kk = wk.k ? wk.k : 1u;
+            s_k[j] = (uint8_t)kk;
+            s_mem[par][j] = (uint8_t)hh_mem_init(j);
+            STAMP(2);
 
-        // live lanes for the entering state, their run entries and offsets
-        const uint32_t st_in = (uint32_t)s_bc[0];
-        const uint32_t d_t = hh_state_d(st_in);
-        const int32_t dprev = hh_state_delta(st_in);
-        const bool live = (mem >> d_t) & 1u;
-        if (live && j + kk < HH_NR) {
-            s_ein[j + kk] = (j + kk) * S + wk.e;
-            s_din[j + kk] = (int16_t)wk.delta;
-        }
-        __syncthreads();
-        const uint32_t e_in = j == d_t ? d_t * S + hh_state_e(st_in) : s_ein[j];
-        const int32_t d_in = j == d_t ? dprev : (int32_t)s_din[j];
-        const uint32_t rc = live ? (uint32_t)((int32_t)(n + wk.cov) + d_in) : 0u;
-        int32_t Tout_i;
-        const uint32_t L = (uint32_t)block_excl_scan((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
-        const uint32_t Tout = (uint32_t)Tout_i;
-        const uint64_t tab_t = s_tab[d_t];
-        uint32_t p = live ? e_in : 0u;
-        const uint32_t y = (j + kk) * S + wk.e;
-        const uint32_t pe = live ? (y < bt ? y : bt) : 0u;
-        uint32_t o = L;
-        STAMP(4);
-
-        uint64_t P0 = 0;
-        for (uint32_t wlo = 0; wlo < Tout || wlo == 0; wlo += geo.ob) {
-            const uint32_t whi = wlo + geo.ob;
-            // pass 2: this lane's symbols with output index in [wlo, whi)
-            if (p < pe && o < whi) {
-                uint32_t val, k;
-                while ((o & 3u) && p < pe && o < whi) {        // head: align to a dword
-                    const uint32_t ha = (o + 3u) & ~3u;
-                    p += hh_emit_step(&c, p, pe, o, ha < whi ? ha : whi, &val, &k);
-                    for (uint32_t i = 0; i < k; i++) s_out[o - wlo + i] = (uint8_t)(val >> (8 * i));
-                    o += k;
+            // transfer table: live masks (exceptions, ascending, by one lane),
+            // charged count and leaving state for every entering d
+            const uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt);   // barriers inside
+            if (j == 0) {
+                for (uint32_t i = 0; i < nexc; i++) {
+                    const uint32_t e = s_exc[i], ke = s_k[e];
+                    const uint8_t m = s_mem[par][e];
+                    for (uint32_t q = e + 1; q < e + ke && q < HH_NR; q++) s_mem[par][q] &= (uint8_t)~m;
                 }
-                uint64_t acc = 0;
-                uint32_t nacc = 0;
-                while (p < pe && o + nacc < whi) {
-                    p += hh_emit_step(&c, p, pe, o + nacc, whi, &val, &k);
-                    acc |= (uint64_t)val << (8 * nacc);
-                    nacc += k;
-                    if (nacc >= 4) {
-                        *(uint32_t *)(s_out + (o - wlo)) = (uint32_t)acc;
-                        acc >>= 32;
-                        nacc -= 4;
-                        o += 4;
-                    }
-                }
-                for (uint32_t i = 0; i < nacc; i++) s_out[o - wlo + i] = (uint8_t)(acc >> (8 * i));
-                o += nacc;
             }
             __syncthreads();
-            STAMP(5);
+            const uint32_t mem = s_mem[par][j];
+            const int32_t charged = (int32_t)(n + wk.cov) + wk.delta;
+            if (j + kk >= HH_NR) {
+                const uint32_t os = hh_state_pack(j + kk - HH_NR, wk.e, wk.delta);
+#pragma unroll
+                for (uint32_t d = 0; d < HH_KM; d++)
+                    if ((mem >> d) & 1u) s_ost[d] = os;
+            }
+#pragma unroll
+            for (uint32_t d = 0; d < HH_KM; d++) {
+                const int32_t v = wave_sum(((mem >> d) & 1u) ? charged : 0);
+                if ((j & 63u) == 0) s_part[j >> 6][d] = v;
+            }
+            __syncthreads();
+            if (j < HH_KM) {
+                int32_t cnt = 0;
+#pragma unroll
+                for (uint32_t w = 0; w < HH_NL / 64; w++) cnt += s_part[w][j];
+                const uint64_t row = hh_tab_pack(cnt, s_ost[j]);
+                s_tab[par][j] = row;
+                if (j > 0) st_sc1(&lb.tabs[tn * HH_KM + j], HH_AGG | row);
+            }
+            __syncthreads();
+            if (j == 0) {
+                // aggregate = table row d = 0 (+ CONST: the leaving state is
+                // the same for every entering d)
+                bool cst = true;
+                for (uint32_t d = 1; d < HH_KM; d++)
+                    cst = cst && hh_tab_state(s_tab[par][d]) == hh_tab_state(s_tab[par][0]);
+                st_sc1(&lb.agg[tn], HH_AGG | (cst ? HH_CST : 0ull) | s_tab[par][0]);
+            }
+            rn.n = n; rn.k = kk; rn.e = wk.e; rn.cov = wk.cov; rn.delta = wk.delta;
+            STAMP(3);
+        }
 
-            if (wlo == 0) {
-                // output base: decoupled look-back over the predecessors
-                if (j < 64) {
-                    const uint64_t excl = t > 0 ? lookback_excl(lb, t, flags) : 0ull;
-                    if (j == 0) {
-                        const uint64_t incl = excl + (uint64_t)(int64_t)hh_tab_count(tab_t);
-                        st_sc1(&lb.inc[t], hh_inc_pack(incl, hh_tab_state(tab_t)));
-                        const uint64_t base = excl - (uint64_t)(int64_t)dprev;
-                        s_bc[1] = base;
-                        if (t == geo.ntiles - 1) {
-                            const uint64_t tot = base + Tout;
-                            flags[2] = (uint32_t)tot;
-                            flags[3] = (uint32_t)(tot >> 32);
-                        }
-                        if (base + Tout > cap) atomicOr(flags, (uint32_t)F_OVER);
-                        if (lb.tdbg) {
-                            lb.tdbg[t * 8 + 0] = base;
-                            lb.tdbg[t * 8 + 1] = Tout | ((uint64_t)st_in << 32);
-                            lb.tdbg[t * 8 + 2] = excl;
-                            lb.tdbg[t * 8 + 3] = tab_t;
+        if (back) {
+            // ---------------- back half of tile tp ----------------
+            const uint32_t pb = par ^ 1u;
+            c.w = s_wb + pb * SW * HH_NLS;
+            const uint64_t rem = geo.bits - tp * tile_bits;
+            c.bt = rem < span ? (uint32_t)rem : span;
+            const uint32_t bt = c.bt;
+            // the state entering tp (published one iteration ago)
+            if (j == 0) s_bc[0] = entering_state(lb, tp, flags);
+            __syncthreads();
+            const uint32_t mem = s_mem[pb][j];
+            const uint32_t st_in = (uint32_t)s_bc[0];
+            const uint32_t d_t = hh_state_d(st_in);
+            const int32_t dprev = hh_state_delta(st_in);
+            const bool live = (mem >> d_t) & 1u;
+            if (live && j + rp.k < HH_NR) {
+                s_ein[j + rp.k] = (j + rp.k) * S + rp.e;
+                s_din[j + rp.k] = (int16_t)rp.delta;
+            }
+            __syncthreads();
+            const uint32_t e_in = j == d_t ? d_t * S + hh_state_e(st_in) : s_ein[j];
+            const int32_t d_in = j == d_t ? dprev : (int32_t)s_din[j];
+            const uint32_t rc = live ? (uint32_t)((int32_t)(rp.n + rp.cov) + d_in) : 0u;
+            int32_t Tout_i;
+            const uint32_t L = (uint32_t)block_excl_scan((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
+            const uint32_t Tout = (uint32_t)Tout_i;
+            const uint64_t tab_t = s_tab[pb][d_t];
+            hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
+            const uint32_t y = (j + rp.k) * S + rp.e;
+            const uint32_t pe = live ? (y < bt ? y : bt) : 0u;
+            uint32_t o = L;
+            STAMP(4);
+
+            uint64_t P0 = 0;
+            for (uint32_t wlo = 0; wlo < Tout || wlo == 0; wlo += geo.ob) {
+                const uint32_t whi = wlo + geo.ob;
+                // pass 2: this lane's symbols with output index in [wlo, whi)
+                if (cu.p < pe && o < whi) {
+                    uint32_t val, k;
+                    while ((o & 3u) && cu.p < pe && o < whi) {     // head: align to a dword
+                        const uint32_t ha = (o + 3u) & ~3u;
+                        hh_emit_step(&c, cu, pe, o, ha < whi ? ha : whi, &val, &k);
+                        for (uint32_t i = 0; i < k; i++) s_out[o - wlo + i] = (uint8_t)(val >> (8 * i));
+                        o += k;
+                    }
+                    uint64_t acc = 0;
+                    uint32_t nacc = 0;
+                    while (cu.p < pe && o + nacc < whi) {
+                        hh_emit_step(&c, cu, pe, o + nacc, whi, &val, &k);
+                        acc |= (uint64_t)val << (8 * nacc);
+                        nacc += k;
+                        if (nacc >= 4) {
+                            *(uint32_t *)(s_out + (o - wlo)) = (uint32_t)acc;
+                            acc >>= 32;
+                            nacc -= 4;
+                            o += 4;
                         }
                     }
+                    for (uint32_t i = 0; i < nacc; i++) s_out[o - wlo + i] = (uint8_t)(acc >> (8 * i));
+                    o += nacc;
                 }
                 __syncthreads();
-                P0 = s_bc[1];
-                STAMP(6);
-            }
+                STAMP(5);
 
-            // copy the window to HBM: 16-B aligned chunks, ragged ends bytewise
-            const uint32_t nr = Tout - wlo < geo.ob ? Tout - wlo : geo.ob;
-            const uint64_t G = P0 + wlo;
-            if (G + nr <= cap && nr > 0) {
-                const uint64_t c0 = G >> 4, c1 = (G + nr + 15) >> 4;
-                for (uint64_t ch = c0 + j; ch < c1; ch += HH_NL) {
-                    const uint64_t a0 = ch << 4;
-                    if (a0 >= G && a0 + 16 <= G + nr) {
-                        const uint32_t s = (uint32_t)(a0 - G);
-                        const uint32_t *d = (const uint32_t *)(s_out + (s & ~3u));
-                        const uint32_t sh = (s & 3u) * 8u;
-                        const uint32_t w0 = d[0], w1 = d[1], w2 = d[2], w3 = d[3], w4 = d[4];
-                        u32x4 q;
-                        q.x = __builtin_amdgcn_alignbit(w1, w0, sh);
-                        q.y = __builtin_amdgcn_alignbit(w2, w1, sh);
-                        q.z = __builtin_amdgcn_alignbit(w3, w2, sh);
-                        q.w = __builtin_amdgcn_alignbit(w4, w3, sh);
-                        __builtin_nontemporal_store(q, (u32x4 *)(out + a0));
-                    } else {
-                        const uint64_t lo = a0 > G ? a0 : G;
-                        const uint64_t hi = a0 + 16 < G + nr ? a0 + 16 : G + nr;
-                        for (uint64_t a = lo; a < hi; a++) out[a] = s_out[a - G];
+                if (wlo == 0) {
+                    // output base: decoupled look-back over the predecessors
+                    if (j < 64) {
+                        const uint64_t excl = tp > 0 ? lookback_excl(lb, tp, flags) : 0ull;
+                        if (j == 0) {
+                            const uint64_t incl = excl + (uint64_t)(int64_t)hh_tab_count(tab_t);
+                            st_sc1(&lb.inc[tp], hh_inc_pack(incl, hh_tab_state(tab_t)));
+                            const uint64_t base = excl - (uint64_t)(int64_t)dprev;
+                            s_bc[1] = base;
+                            if (tp == geo.ntiles - 1) {
+                                const uint64_t tot = base + Tout;
+                                flags[2] = (uint32_t)tot;
+                                flags[3] = (uint32_t)(tot >> 32);
+                            }
+                            if (base + Tout > cap) atomicOr(flags, (uint32_t)F_OVER);
+                            if (lb.tdbg) {
+                                lb.tdbg[tp * 8 + 0] = base;
+                                lb.tdbg[tp * 8 + 1] = Tout | ((uint64_t)st_in << 32);
+                                lb.tdbg[tp * 8 + 2] = excl;
+                                lb.tdbg[tp * 8 + 3] = tab_t;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                    P0 = s_bc[1];
+                    STAMP(6);
+                }
+
+                // copy the window to HBM: 16-B aligned chunks, ragged ends bytewise
+                const uint32_t nr = Tout - wlo < geo.ob ? Tout - wlo : geo.ob;
+                const uint64_t Gb = P0 + wlo;
+                if (Gb + nr <= cap && nr > 0) {
+                    const uint64_t c0 = Gb >> 4, c1 = (Gb + nr + 15) >> 4;
+                    for (uint64_t ch = c0 + j; ch < c1; ch += HH_NL) {
+                        const uint64_t a0 = ch << 4;
+                        if (a0 >= Gb && a0 + 16 <= Gb + nr) {
+                            const uint32_t s = (uint32_t)(a0 - Gb);
+                            const uint32_t *d = (const uint32_t *)(s_out + (s & ~3u));
+                            const uint32_t sh = (s & 3u) * 8u;
+                            const uint32_t w0 = d[0], w1 = d[1], w2 = d[2], w3 = d[3], w4 = d[4];
+                            u32x4 q;
+                            q.x = __builtin_amdgcn_alignbit(w1, w0, sh);
+                            q.y = __builtin_amdgcn_alignbit(w2, w1, sh);
+                            q.z = __builtin_amdgcn_alignbit(w3, w2, sh);
+                            q.w = __builtin_amdgcn_alignbit(w4, w3, sh);
+                            __builtin_nontemporal_store(q, (u32x4 *)(out + a0));
+                        } else {
+                            const uint64_t lo = a0 > Gb ? a0 : Gb;
+                            const uint64_t hi = a0 + 16 < Gb + nr ? a0 + 16 : Gb + nr;
+                            for (uint64_t a = lo; a < hi; a++) out[a] = s_out[a - Gb];
+                        }
                     }
                 }
+                STAMP(7);
+                if (wlo + geo.ob >= Tout) break;
+                __syncthreads();            // window copied before the next round
             }
-            STAMP(7);
-            if (wlo + geo.ob >= Tout) break;
-            __syncthreads();            // window copied before the next round
         }
+        // the front half's tile becomes the pending one
+        rp = rn;
+        tp = front ? tn : ~0ull;
+        tn = front ? tn + G : tn;
+        par ^= 1u;
     }
     STAMP_FLUSH(dbg);
 }
@@ -793,7 +837,7 @@ static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8
                           uint64_t cap, uint64_t *out_len, hipStream_t st);
 
 static size_t lds_bytes(const hh_decoder *d) {
-    return (size_t)HH_L1_SIZE * 8 + (size_t)(d->S / 32) * HH_NLS * 4 + d->ob + 16 +
+    return (size_t)HH_L1_SIZE * 8 + 3 * (size_t)(d->S / 32) * HH_NLS * 4 + d->ob + 16 +
            (size_t)d->tab.l2_used * 4;
 }
 
@@ -857,13 +901,14 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     geo.sw = d->S / 32;
     geo.magic = hh_magic(geo.sw);
     geo.ob = d->ob;
+    geo.maxadv = d->ht->maxlen > HH_P ? (uint32_t)d->ht->maxlen : HH_P;
     geo.nwords = ((bits + 7) / 8 + HH_PAYLOAD_PAD) / 4;
     const uint64_t tb = (uint64_t)HH_NR * d->S;
     geo.ntiles = (bits + tb - 1) / tb;
     geo.vec4 = (((uintptr_t)d_data & 15u) == 0) && (geo.sw % 4 == 0);
-    // workspace: [flags 64 B | agg[ntiles] | inc[ntiles]] (zeroed)
+    // workspace: [flags 64 B | agg[ntiles] | inc[ntiles] | tabs[ntiles][KM]] (zeroed)
     //            | (HH_DEBUG_TILES) tdbg[ntiles][8]
-    const size_t zero_bytes = 64 + (size_t)geo.ntiles * 16;
+    const size_t zero_bytes = 64 + (size_t)geo.ntiles * (16 + 8 * HH_KM);
     const int dbg_tiles = getenv("HH_DEBUG_TILES") != nullptr;
     int rc = ensure_ws(d, zero_bytes + (size_t)geo.ntiles * (dbg_tiles ? 8 : 0) * 8 + 256);
     if (rc) return rc;
@@ -872,7 +917,8 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     LookBack lb;
     lb.agg = (uint64_t *)(w + 64);
     lb.inc = lb.agg + geo.ntiles;
-    lb.tdbg = dbg_tiles ? lb.inc + geo.ntiles : nullptr;
+    lb.tabs = lb.inc + geo.ntiles;
+    lb.tdbg = dbg_tiles ? lb.tabs + geo.ntiles * HH_KM : nullptr;
     d->last_ntiles = geo.ntiles;
     const size_t lds = lds_bytes(d);
     const kdec_t kf = kdec_for(geo.sw);
@@ -1088,7 +1134,7 @@ extern "C" int hh_debug_tiles(hh_decoder *d, uint64_t *out, int max_tiles) {
     if (!d || !out || !d->ws || !getenv("HH_DEBUG_TILES")) return 0;
     const uint64_t nt = d->last_ntiles;
     const int n = (int)(nt < (uint64_t)max_tiles ? nt : (uint64_t)max_tiles);
-    const uint64_t *src = (const uint64_t *)((uint8_t *)d->ws + 64) + nt * 2;
+    const uint64_t *src = (const uint64_t *)((uint8_t *)d->ws + 64) + nt * (2 + HH_KM);
     if (hipMemcpy(out, src, (size_t)n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         return HH_ERR_DEVICE;
     return n;

@@ -49,6 +49,8 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
     const uint32_t span = HH_NCOL * S;
     std::vector<uint32_t> w((size_t)sw * HH_NLS);
     std::vector<uint32_t> xs(HH_NR), ns(HH_NR), mem(HH_NR), ent(HH_NR);
+    std::vector<uint16_t> n16(HH_NR);
+    std::vector<uint32_t> mk((size_t)sw * HH_NLS);   // boundary masks (transposed like w)
     std::vector<int32_t> din(HH_NR);
     std::vector<hh_wk> wk(HH_NR);
     stats[0] = (int64_t)ntiles;
@@ -77,21 +79,25 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
         c.l2 = T.l2;
         c.tree = T.tree;
         c.tsym = T.tsym;
+        c.maxadv = T.maxlen > HH_P ? (uint32_t)T.maxlen : HH_P;
         const uint64_t rem = bits - t * TB;
         c.bt = rem < span ? (uint32_t)rem : span;
         const uint32_t bt = c.bt;
 
+        for (size_t i = 0; i < mk.size(); i++)          // words pass 1 leaves unwritten
+            mk[i] = (uint32_t)(0x9e3779b9u * (uint32_t)(i + t * 7919u + 1));   // hold junk
         for (uint32_t j = 0; j < HH_NR; j++) {            // pass 1
             uint32_t p0 = j * S, n = 0, x = bt;
             if (p0 < bt) {
                 uint32_t lim = p0 + S < bt ? p0 + S : bt;
-                x = hh_region_count(&c, p0, lim, &n);
+                x = hh_region_count(&c, p0, lim, &n, mk.data());
             }
             xs[j] = x;
             ns[j] = n;
+            n16[j] = (uint16_t)n;
         }
         for (uint32_t j = 0; j < HH_NR; j++) {            // walks
-            wk[j] = hh_walk(&c, j, S, xs[j]);
+            wk[j] = hh_walk(&c, j, S, xs[j], mk.data(), xs.data(), n16.data(), HH_NR);
             if (wk[j].k == 0) stats[2]++;
             if (wk[j].k > 1) stats[1]++;
             if ((int64_t)wk[j].k > stats[4]) stats[4] = wk[j].k;
@@ -143,20 +149,20 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
             const uint32_t pe0 = (j + wk[j].k) * S + wk[j].e;
             const uint32_t pe = pe0 < bt ? pe0 : bt;
             const uint64_t want = (uint64_t)((int64_t)ns[j] + wk[j].cov + din[j]);
-            uint32_t p = ent[j];
+            hh_cur cu = hh_cur_at(&c, ent[j]);
             const uint64_t o0 = o;
-            while (p < pe) {
+            while (cu.p < pe) {
                 uint32_t val, k;
-                p += hh_emit_step(&c, p, pe, o, ~0ull, &val, &k);
+                hh_emit_step(&c, cu, pe, o, ~0ull, &val, &k);
                 for (uint32_t i = 0; i < k; i++) {
                     if (o + i >= cap) return HH_ERR_CAPACITY;
                     out[o + i] = (uint8_t)(val >> (8 * i));
                 }
                 o += k;
             }
-            if (o - o0 != want || (p != pe && !(p >= pe && ent[j] >= pe))) {
+            if (o - o0 != want || (cu.p != pe && !(cu.p >= pe && ent[j] >= pe))) {
                 fprintf(stderr, "emu: tile %lu lane %u emitted %lu, predicted %lu (e=%u pe=%u p=%u)\n",
-                        (unsigned long)t, j, (unsigned long)(o - o0), (unsigned long)want, ent[j], pe, p);
+                        (unsigned long)t, j, (unsigned long)(o - o0), (unsigned long)want, ent[j], pe, cu.p);
                 return HH_ERR_INTERNAL;
             }
         }
@@ -174,12 +180,13 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
             // the kernel's pass 2 exactly: per-lane (p, o) carried across
             // output windows of g_ob bytes, head bytes to a dword boundary,
             // dword writes, tail bytes; then the window copy
-            std::vector<uint32_t> P(HH_NR), PE(HH_NR), OO(HH_NR);
+            std::vector<hh_cur> P(HH_NR);
+            std::vector<uint32_t> PE(HH_NR), OO(HH_NR);
             uint32_t L = 0;
             for (uint32_t j = 0; j < HH_NR; j++) {
                 const bool live = (mem[j] >> d_t) & 1u;
                 const uint32_t y = (j + wk[j].k) * S + wk[j].e;
-                P[j] = live ? ent[j] : 0u;
+                P[j] = hh_cur_at(&c, live ? ent[j] : 0u);
                 PE[j] = live ? (y < bt ? y : bt) : 0u;
                 OO[j] = L;
                 L += live ? (uint32_t)((int64_t)ns[j] + wk[j].cov + din[j]) : 0u;
@@ -189,20 +196,21 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
                 const uint32_t whi = wlo + g_ob;
                 std::fill(win.begin(), win.end(), 0xAB);
                 for (uint32_t j = 0; j < HH_NR; j++) {
-                    uint32_t &p = P[j], &oo = OO[j];
+                    hh_cur &cu = P[j];
+                    uint32_t &oo = OO[j];
                     const uint32_t pe = PE[j];
-                    if (!(p < pe && oo < whi)) continue;
+                    if (!(cu.p < pe && oo < whi)) continue;
                     uint32_t val, k;
-                    while ((oo & 3u) && p < pe && oo < whi) {
+                    while ((oo & 3u) && cu.p < pe && oo < whi) {
                         const uint32_t ha = (oo + 3u) & ~3u;
-                        p += hh_emit_step(&c, p, pe, oo, ha < whi ? ha : whi, &val, &k);
+                        hh_emit_step(&c, cu, pe, oo, ha < whi ? ha : whi, &val, &k);
                         for (uint32_t i = 0; i < k; i++) win[oo - wlo + i] = (uint8_t)(val >> (8 * i));
                         oo += k;
                     }
                     uint64_t acc = 0;
                     uint32_t nacc = 0;
-                    while (p < pe && oo + nacc < whi) {
-                        p += hh_emit_step(&c, p, pe, oo + nacc, whi, &val, &k);
+                    while (cu.p < pe && oo + nacc < whi) {
+                        hh_emit_step(&c, cu, pe, oo + nacc, whi, &val, &k);
                         acc |= (uint64_t)val << (8 * nacc);
                         nacc += k;
                         if (nacc >= 4) {
