@@ -61,11 +61,15 @@
 /*   (HH_NLS is a multiple of 32) however far apart the lanes' chains    */
 /*   are.                                                                */
 /* ------------------------------------------------------------------ */
+#ifndef HH_NL
 #define HH_NL 256
+#endif
 #define HH_NR HH_NL           /* regions per tile */
 #define HH_KM 8               /* max regions one walk may cross */
 #define HH_NCOL (HH_NR + HH_KM + 1)   /* staged columns */
+#ifndef HH_NLS
 #define HH_NLS 288            /* >= HH_NCOL, multiple of 32 */
+#endif
 #define HH_SW_MAX 12          /* max words per region (S <= 384) */
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
                                  as a failed walk) */
@@ -85,13 +89,21 @@ HH_HD uint32_t hh_popc(uint32_t v) { return (uint32_t)__builtin_popcount(v); }
 HH_HD uint32_t hh_lowmask(uint32_t o) { return o >= 32 ? 0xffffffffu : ((1u << o) - 1u); }
 
 /* ceil(2^32 / sw): hh_umulhi(g, magic) == g / sw exactly for g < 2^20. */
+/* fields of the meta half of an L1 entry (hh_internal.h bits 32..55) */
+#define HH_M_NBITS(m) ((m) & 31u)
+#define HH_M_NSYM(m) (((m) >> 5) & 7u)
+#define HH_M_LEN0(m) (((m) >> 8) & 31u)
+#define HH_M_BMASK(m) (((m) >> 13) & 0x7ffu)
+
 HH_HD uint32_t hh_magic(uint32_t sw) { return (uint32_t)((0x100000000ull + sw - 1) / sw); }
 
 typedef struct {
     const uint32_t *w;    /* transposed tile words                        */
     uint32_t sw;          /* words per region                             */
     uint32_t magic;       /* hh_magic(sw)                                 */
-    const uint64_t *l1;   /* HH_L1_SIZE entries                           */
+    const uint32_t *l1m;  /* HH_L1_SIZE entries: the meta half (bits 32..63
+                             of the hh_internal.h L1 entry; HH_M_*)      */
+    const uint32_t *l1s;  /* the symbol half (bits 0..31; escape: L2 ref) */
     const uint32_t *l2;
     const uint32_t *tree; /* compact tree (tail symbols, very long codes) */
     const uint8_t *tsym;
@@ -154,8 +166,8 @@ HH_HD uint32_t hh_tail_symbol(const hh_ctx *c, uint32_t p) {
 /* First code longer than HH_P bits: second-level table, then (very long
  * codes only) a bit-serial walk.  Returns the code length.  A walk that
  * hits the end of the stream returns the cut-off length. */
-HH_HD uint32_t hh_escape(const hh_ctx *c, uint32_t p, uint32_t win, uint64_t e,
-                         uint32_t *sym) {
+HH_HD uint32_t hh_escape(const hh_ctx *c, uint32_t p, uint32_t win, uint32_t *sym) {
+    const uint32_t e = c->l1s[win & (HH_L1_SIZE - 1u)];
     uint32_t q = HH_L1_L2Q(e), base = HH_L1_L2BASE(e);
     uint32_t e2 = c->l2[base + ((win >> HH_P) & ((1u << q) - 1u))];
     if (e2 & HH_L2_LEAF) {
@@ -181,17 +193,17 @@ typedef struct {
 } hh_look;
 
 HH_HD hh_look hh_lookup_w(const hh_ctx *c, uint32_t p, uint32_t win) {
-    uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
+    const uint32_t m = c->l1m[win & (HH_L1_SIZE - 1u)];
     hh_look L;
-    L.ns = HH_L1_NSYM(e);
+    L.ns = HH_M_NSYM(m);
     if (L.ns) {
-        L.nb = HH_L1_NBITS(e);
-        L.bm = HH_L1_BMASK(e);
-        L.len0 = HH_L1_LEN0(e);
-        L.syms = HH_L1_SYMS(e);
+        L.nb = HH_M_NBITS(m);
+        L.bm = HH_M_BMASK(m);
+        L.len0 = HH_M_LEN0(m);
+        L.syms = c->l1s[win & (HH_L1_SIZE - 1u)];
     } else {
         uint32_t s;
-        L.nb = L.len0 = hh_escape(c, p, win, e, &s);
+        L.nb = L.len0 = hh_escape(c, p, win, &s);
         L.ns = 1;
         L.bm = 1;
         L.syms = s;
@@ -258,11 +270,11 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
     const uint32_t lf = lim > c->maxadv ? lim - c->maxadv : 0u;
     while (u.p < lf) {
         const uint32_t win = hh_cur_win(u);
-        const uint64_t e = c->l1[win & (HH_L1_SIZE - 1u)];
-        uint32_t ns = HH_L1_NSYM(e), nb = HH_L1_NBITS(e), bm = HH_L1_BMASK(e);
+        const uint32_t m = c->l1m[win & (HH_L1_SIZE - 1u)];
+        uint32_t ns = HH_M_NSYM(m), nb = HH_M_NBITS(m), bm = HH_M_BMASK(m);
         if (ns == 0) {
             uint32_t s;
-            nb = hh_escape(c, u.p, win, e, &s);
+            nb = hh_escape(c, u.p, win, &s);
             ns = 1;
             bm = 1;
         }

@@ -32,7 +32,6 @@
 #include "hh_internal.h"
 #include "hiphuff.h"
 
-#define HH_OB_DEFAULT (16u << 10)   // LDS output window per workgroup (bytes)
 #define HH_MAXLEN_FAST 32           // longest code of the fast path (one cursor step <= 32 bits)
 
 #define HIP_OK(x)                                                             \
@@ -206,7 +205,10 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flag
             for (uint32_t i = 0; i < V; i++) {
                 const uint32_t o = lane * V + i;
                 if (o < ofirst) {
-                    const bool pin = o + 1 == ofirst;
+                    // pinned to the inclusive granule found (none in this
+                    // window: the last tile's state comes from its
+                    // predecessor's aggregate, av[V], like every other)
+                    const bool pin = o + 1 == ofirst && ofirst < 64u * V;
                     const uint64_t pv = av[i + 1];
                     const bool known = pin || ((pv >> HH_ST_SHIFT) != 0 && (pv & HH_CST));
                     const uint32_t d = hh_state_d(pin ? hh_inc_state(incv) : hh_tab_state(pv));
@@ -320,7 +322,6 @@ struct Geometry {
     uint64_t nwords;     // readable payload words
     uint64_t ntiles;
     uint32_t S, sw, magic;
-    uint32_t ob;         // LDS output window bytes (multiple of 16)
     uint32_t vec4;       // 16-B aligned payload and sw % 4 == 0
     uint32_t maxadv;     // max(HH_P, longest code)
 };
@@ -354,11 +355,11 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     __shared__ uint16_t s_n[HH_NR];
 
     constexpr uint32_t S = 32 * SW;
-    uint64_t *s_l1 = (uint64_t *)smem;
+    uint32_t *s_l1m = (uint32_t *)smem;                          // L1 meta halves
+    uint32_t *s_l1s = s_l1m + HH_L1_SIZE;                        // L1 symbol halves
     uint32_t *s_wb = (uint32_t *)(smem + HH_L1_SIZE * 8);       // 2 x SW * HH_NLS words
     uint32_t *s_mk = s_wb + 2 * SW * HH_NLS;                     // SW * HH_NLS boundary-mask words
-    uint8_t *s_out = (uint8_t *)(s_mk + SW * HH_NLS);
-    uint32_t *s_l2 = (uint32_t *)(s_out + geo.ob + 16);
+    uint32_t *s_l2 = s_mk + SW * HH_NLS;
 
     const uint32_t j = threadIdx.x;
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
@@ -366,13 +367,18 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     const uint64_t G = gridDim.x;
     STAMP_DECL
 
-    for (uint32_t i = j; i < HH_L1_SIZE; i += HH_NL) s_l1[i] = tab.l1[i];
+    for (uint32_t i = j; i < HH_L1_SIZE; i += HH_NL) {
+        const uint64_t e = tab.l1[i];
+        s_l1m[i] = (uint32_t)(e >> 32);
+        s_l1s[i] = (uint32_t)e;
+    }
     for (uint32_t i = j; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
 
     hh_ctx c;
     c.sw = SW;
     c.magic = 0;
-    c.l1 = s_l1;
+    c.l1m = s_l1m;
+    c.l1s = s_l1s;
     c.l2 = s_l2;
     c.tree = tab.tree;
     c.tsym = tab.tsym;
@@ -488,113 +494,80 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             const uint32_t st_in = (uint32_t)s_bc[0];
             const uint32_t d_t = hh_state_d(st_in);
             const int32_t dprev = hh_state_delta(st_in);
+            const uint64_t tab_t = s_tab[pb][d_t];
             const bool live = (mem >> d_t) & 1u;
             if (live && j + rp.k < HH_NR) {
                 s_ein[j + rp.k] = (j + rp.k) * S + rp.e;
                 s_din[j + rp.k] = (int16_t)rp.delta;
             }
+            if (j < 64) {
+                // output base: decoupled look-back over the predecessors
+                const uint64_t excl = tp > 0 ? lookback_excl(lb, tp, flags) : 0ull;
+                if (j == 0) {
+                    const uint64_t incl = excl + (uint64_t)(int64_t)hh_tab_count(tab_t);
+                    st_sc1(&lb.inc[tp], hh_inc_pack(incl, hh_tab_state(tab_t)));
+                    s_bc[1] = excl - (uint64_t)(int64_t)dprev;
+                    if (lb.tdbg) {
+                        lb.tdbg[tp * 8 + 2] = excl;
+                        lb.tdbg[tp * 8 + 3] = tab_t;
+                    }
+                }
+            }
             __syncthreads();
+            STAMP(4);
             const uint32_t e_in = j == d_t ? d_t * S + hh_state_e(st_in) : s_ein[j];
             const int32_t d_in = j == d_t ? dprev : (int32_t)s_din[j];
             const uint32_t rc = live ? (uint32_t)((int32_t)(rp.n + rp.cov) + d_in) : 0u;
             int32_t Tout_i;
             const uint32_t L = (uint32_t)block_excl_scan((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
             const uint32_t Tout = (uint32_t)Tout_i;
-            const uint64_t tab_t = s_tab[pb][d_t];
+            const uint64_t P0 = s_bc[1];
+            if (j == 0) {
+                if (tp == geo.ntiles - 1) {
+                    const uint64_t tot = P0 + Tout;
+                    flags[2] = (uint32_t)tot;
+                    flags[3] = (uint32_t)(tot >> 32);
+                }
+                if (P0 + Tout > cap) atomicOr(flags, (uint32_t)F_OVER);
+                if (lb.tdbg) {
+                    lb.tdbg[tp * 8 + 0] = P0;
+                    lb.tdbg[tp * 8 + 1] = Tout | ((uint64_t)st_in << 32);
+                }
+            }
+            STAMP(5);
+
+            // pass 2: this lane's symbols, straight to HBM (output bytes
+            // [P0 + L, P0 + L + rc)); bytes up to a dword boundary, then
+            // dwords, then the ragged end
             hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
             const uint32_t y = (j + rp.k) * S + rp.e;
-            const uint32_t pe = live ? (y < bt ? y : bt) : 0u;
-            uint32_t o = L;
-            STAMP(4);
-
-            uint64_t P0 = 0;
-            for (uint32_t wlo = 0; wlo < Tout || wlo == 0; wlo += geo.ob) {
-                const uint32_t whi = wlo + geo.ob;
-                // pass 2: this lane's symbols with output index in [wlo, whi)
-                if (cu.p < pe && o < whi) {
-                    uint32_t val, k;
-                    while ((o & 3u) && cu.p < pe && o < whi) {     // head: align to a dword
-                        const uint32_t ha = (o + 3u) & ~3u;
-                        hh_emit_step(&c, cu, pe, o, ha < whi ? ha : whi, &val, &k);
-                        for (uint32_t i = 0; i < k; i++) s_out[o - wlo + i] = (uint8_t)(val >> (8 * i));
-                        o += k;
-                    }
-                    uint64_t acc = 0;
-                    uint32_t nacc = 0;
-                    while (cu.p < pe && o + nacc < whi) {
-                        hh_emit_step(&c, cu, pe, o + nacc, whi, &val, &k);
-                        acc |= (uint64_t)val << (8 * nacc);
-                        nacc += k;
-                        if (nacc >= 4) {
-                            *(uint32_t *)(s_out + (o - wlo)) = (uint32_t)acc;
-                            acc >>= 32;
-                            nacc -= 4;
-                            o += 4;
-                        }
-                    }
-                    for (uint32_t i = 0; i < nacc; i++) s_out[o - wlo + i] = (uint8_t)(acc >> (8 * i));
-                    o += nacc;
+            const uint32_t pe = (live && P0 + Tout <= cap) ? (y < bt ? y : bt) : 0u;
+            if (cu.p < pe) {
+                uint8_t *ob = out + P0;
+                uint32_t o = L, val, k;
+                const uint32_t oend = L + rc;
+                while (((P0 + o) & 3u) && cu.p < pe) {
+                    const uint32_t ha = o + (4u - (uint32_t)((P0 + o) & 3u));
+                    hh_emit_step(&c, cu, pe, o, ha, &val, &k);
+                    for (uint32_t i = 0; i < k; i++) ob[o + i] = (uint8_t)(val >> (8 * i));
+                    o += k;
                 }
-                __syncthreads();
-                STAMP(5);
-
-                if (wlo == 0) {
-                    // output base: decoupled look-back over the predecessors
-                    if (j < 64) {
-                        const uint64_t excl = tp > 0 ? lookback_excl(lb, tp, flags) : 0ull;
-                        if (j == 0) {
-                            const uint64_t incl = excl + (uint64_t)(int64_t)hh_tab_count(tab_t);
-                            st_sc1(&lb.inc[tp], hh_inc_pack(incl, hh_tab_state(tab_t)));
-                            const uint64_t base = excl - (uint64_t)(int64_t)dprev;
-                            s_bc[1] = base;
-                            if (tp == geo.ntiles - 1) {
-                                const uint64_t tot = base + Tout;
-                                flags[2] = (uint32_t)tot;
-                                flags[3] = (uint32_t)(tot >> 32);
-                            }
-                            if (base + Tout > cap) atomicOr(flags, (uint32_t)F_OVER);
-                            if (lb.tdbg) {
-                                lb.tdbg[tp * 8 + 0] = base;
-                                lb.tdbg[tp * 8 + 1] = Tout | ((uint64_t)st_in << 32);
-                                lb.tdbg[tp * 8 + 2] = excl;
-                                lb.tdbg[tp * 8 + 3] = tab_t;
-                            }
-                        }
-                    }
-                    __syncthreads();
-                    P0 = s_bc[1];
-                    STAMP(6);
-                }
-
-                // copy the window to HBM: 16-B aligned chunks, ragged ends bytewise
-                const uint32_t nr = Tout - wlo < geo.ob ? Tout - wlo : geo.ob;
-                const uint64_t Gb = P0 + wlo;
-                if (Gb + nr <= cap && nr > 0) {
-                    const uint64_t c0 = Gb >> 4, c1 = (Gb + nr + 15) >> 4;
-                    for (uint64_t ch = c0 + j; ch < c1; ch += HH_NL) {
-                        const uint64_t a0 = ch << 4;
-                        if (a0 >= Gb && a0 + 16 <= Gb + nr) {
-                            const uint32_t s = (uint32_t)(a0 - Gb);
-                            const uint32_t *d = (const uint32_t *)(s_out + (s & ~3u));
-                            const uint32_t sh = (s & 3u) * 8u;
-                            const uint32_t w0 = d[0], w1 = d[1], w2 = d[2], w3 = d[3], w4 = d[4];
-                            u32x4 q;
-                            q.x = __builtin_amdgcn_alignbit(w1, w0, sh);
-                            q.y = __builtin_amdgcn_alignbit(w2, w1, sh);
-                            q.z = __builtin_amdgcn_alignbit(w3, w2, sh);
-                            q.w = __builtin_amdgcn_alignbit(w4, w3, sh);
-                            __builtin_nontemporal_store(q, (u32x4 *)(out + a0));
-                        } else {
-                            const uint64_t lo = a0 > Gb ? a0 : Gb;
-                            const uint64_t hi = a0 + 16 < Gb + nr ? a0 + 16 : Gb + nr;
-                            for (uint64_t a = lo; a < hi; a++) out[a] = s_out[a - Gb];
-                        }
+                uint64_t acc = 0;
+                uint32_t nacc = 0;
+                while (cu.p < pe) {
+                    hh_emit_step(&c, cu, pe, o + nacc, oend, &val, &k);
+                    acc |= (uint64_t)val << (8 * nacc);
+                    nacc += k;
+                    if (nacc >= 4) {
+                        __builtin_nontemporal_store((uint32_t)acc, (uint32_t *)(ob + o));
+                        acc >>= 32;
+                        nacc -= 4;
+                        o += 4;
                     }
                 }
-                STAMP(7);
-                if (wlo + geo.ob >= Tout) break;
-                __syncthreads();            // window copied before the next round
+                for (uint32_t i = 0; i < nacc; i++) ob[o + i] = (uint8_t)(acc >> (8 * i));
             }
+            STAMP(6);
         }
         // the front half's tile becomes the pending one
         rp = rn;
@@ -709,7 +682,6 @@ struct hh_decoder {
     uint8_t *d_tsym;
     DevTab tab;
     uint32_t S;
-    uint32_t ob;
     // workspace
     void *ws;
     size_t ws_size;
@@ -749,11 +721,6 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
     if (hipSetDevice(d->device) != hipSuccess) { free(d); return HH_ERR_DEVICE; }
     d->ht = (hh_tables *)calloc(1, sizeof(hh_tables));
     if (!d->ht) { free(d); return HH_ERR_NOMEM; }
-    d->ob = HH_OB_DEFAULT;
-    if (const char *e = getenv("HH_OB_KIB")) {
-        long v = strtol(e, nullptr, 10);
-        if (v >= 1 && v <= 96) d->ob = (uint32_t)v << 10;
-    }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&d->d_l1, sizeof(uint64_t) * HH_L1_SIZE) != hipSuccess ||
         hipMalloc(&d->d_l2, sizeof(uint32_t) * HH_L2_MAX) != hipSuccess ||
@@ -837,7 +804,7 @@ static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8
                           uint64_t cap, uint64_t *out_len, hipStream_t st);
 
 static size_t lds_bytes(const hh_decoder *d) {
-    return (size_t)HH_L1_SIZE * 8 + 3 * (size_t)(d->S / 32) * HH_NLS * 4 + d->ob + 16 +
+    return (size_t)HH_L1_SIZE * 8 + 3 * (size_t)(d->S / 32) * HH_NLS * 4 +
            (size_t)d->tab.l2_used * 4;
 }
 
@@ -900,7 +867,6 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     geo.S = d->S;
     geo.sw = d->S / 32;
     geo.magic = hh_magic(geo.sw);
-    geo.ob = d->ob;
     geo.maxadv = d->ht->maxlen > HH_P ? (uint32_t)d->ht->maxlen : HH_P;
     geo.nwords = ((bits + 7) / 8 + HH_PAYLOAD_PAD) / 4;
     const uint64_t tb = (uint64_t)HH_NR * d->S;

@@ -22,11 +22,9 @@
 #include "hh_algo.h"
 #include "hiphuff.h"
 
-static uint32_t g_ob = 0;   // > 0: also replay the kernel's windowed pass 2
 
 extern "C" {
 
-void hh_emu_set_window(uint32_t ob) { g_ob = ob; }
 
 // stats[0]=tiles stats[1]=walks with k > 1 stats[2]=failed walks
 // stats[3]=region bits used stats[4]=max k stats[5]=non-CONST tiles
@@ -50,6 +48,11 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
     std::vector<uint32_t> w((size_t)sw * HH_NLS);
     std::vector<uint32_t> xs(HH_NR), ns(HH_NR), mem(HH_NR), ent(HH_NR);
     std::vector<uint16_t> n16(HH_NR);
+    std::vector<uint32_t> l1m(HH_L1_SIZE), l1s(HH_L1_SIZE);   // split L1, as staged in LDS
+    for (uint32_t i = 0; i < HH_L1_SIZE; i++) {
+        l1m[i] = (uint32_t)(T.l1[i] >> 32);
+        l1s[i] = (uint32_t)T.l1[i];
+    }
     std::vector<uint32_t> mk((size_t)sw * HH_NLS);   // boundary masks (transposed like w)
     std::vector<int32_t> din(HH_NR);
     std::vector<hh_wk> wk(HH_NR);
@@ -75,7 +78,8 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
         c.w = w.data();
         c.sw = sw;
         c.magic = hh_magic(sw);
-        c.l1 = T.l1;
+        c.l1m = l1m.data();
+        c.l1s = l1s.data();
         c.l2 = T.l2;
         c.tree = T.tree;
         c.tsym = T.tsym;
@@ -176,63 +180,6 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
                         wk[j].k, wk[j].e, wk[j].cov, wk[j].delta, mem[j]);
         }
         if ((int64_t)(o - base) != tout) return HH_ERR_INTERNAL - 2;
-        if (g_ob) {
-            // the kernel's pass 2 exactly: per-lane (p, o) carried across
-            // output windows of g_ob bytes, head bytes to a dword boundary,
-            // dword writes, tail bytes; then the window copy
-            std::vector<hh_cur> P(HH_NR);
-            std::vector<uint32_t> PE(HH_NR), OO(HH_NR);
-            uint32_t L = 0;
-            for (uint32_t j = 0; j < HH_NR; j++) {
-                const bool live = (mem[j] >> d_t) & 1u;
-                const uint32_t y = (j + wk[j].k) * S + wk[j].e;
-                P[j] = hh_cur_at(&c, live ? ent[j] : 0u);
-                PE[j] = live ? (y < bt ? y : bt) : 0u;
-                OO[j] = L;
-                L += live ? (uint32_t)((int64_t)ns[j] + wk[j].cov + din[j]) : 0u;
-            }
-            std::vector<uint8_t> win(g_ob + 16);
-            for (uint32_t wlo = 0; wlo < L || wlo == 0; wlo += g_ob) {
-                const uint32_t whi = wlo + g_ob;
-                std::fill(win.begin(), win.end(), 0xAB);
-                for (uint32_t j = 0; j < HH_NR; j++) {
-                    hh_cur &cu = P[j];
-                    uint32_t &oo = OO[j];
-                    const uint32_t pe = PE[j];
-                    if (!(cu.p < pe && oo < whi)) continue;
-                    uint32_t val, k;
-                    while ((oo & 3u) && cu.p < pe && oo < whi) {
-                        const uint32_t ha = (oo + 3u) & ~3u;
-                        hh_emit_step(&c, cu, pe, oo, ha < whi ? ha : whi, &val, &k);
-                        for (uint32_t i = 0; i < k; i++) win[oo - wlo + i] = (uint8_t)(val >> (8 * i));
-                        oo += k;
-                    }
-                    uint64_t acc = 0;
-                    uint32_t nacc = 0;
-                    while (cu.p < pe && oo + nacc < whi) {
-                        hh_emit_step(&c, cu, pe, oo + nacc, whi, &val, &k);
-                        acc |= (uint64_t)val << (8 * nacc);
-                        nacc += k;
-                        if (nacc >= 4) {
-                            memcpy(&win[oo - wlo], &acc, 4);
-                            acc >>= 32;
-                            nacc -= 4;
-                            oo += 4;
-                        }
-                    }
-                    for (uint32_t i = 0; i < nacc; i++) win[oo - wlo + i] = (uint8_t)(acc >> (8 * i));
-                    oo += nacc;
-                }
-                const uint32_t nr = L - wlo < g_ob ? L - wlo : g_ob;
-                for (uint32_t i = 0; i < nr; i++)
-                    if (win[i] != out[base + wlo + i]) {
-                        fprintf(stderr, "emu: window mismatch tile %lu byte %u (window %u)\n",
-                                (unsigned long)t, wlo + i, wlo);
-                        return HH_ERR_INTERNAL - 3;
-                    }
-                if (wlo + g_ob >= L) break;
-            }
-        }
         excl += cnt[d_t];
         base = o;
         st_in = so;
