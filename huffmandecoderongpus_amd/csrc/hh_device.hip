@@ -384,8 +384,14 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     c.tsym = tab.tsym;
     c.maxadv = geo.maxadv;
 
+    // Tiles are claimed in order from a counter one iteration before their
+    // front half (the first two per workgroup are blockIdx.x and +G), so the
+    // predecessors of a tile entering its back half were claimed earlier and
+    // normally have their aggregates published: no convoy behind a slow
+    // workgroup as with a fixed stride.
     Prefetch pf;
     uint64_t tn = blockIdx.x;                   // tile for the next front half
+    uint64_t tq = blockIdx.x + G;               // tile prefetched during that front half
     if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
 
     LaneRec rp = {0u, 1u, 0u, 0u, 0};           // the pending tile (front done)
@@ -405,7 +411,8 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             c.bt = rem < span ? (uint32_t)rem : span;
             const uint32_t bt = c.bt;
             store_tile<SW>(pf, s_w);
-            if (tn + G < geo.ntiles) prefetch_tile<SW>(pf, gdata, (tn + G) * tile_bits / 32, geo.nwords, geo.vec4);
+            if (tq < geo.ntiles) prefetch_tile<SW>(pf, gdata, tq * tile_bits / 32, geo.nwords, geo.vec4);
+            if (j == 0 && tq < geo.ntiles) s_bc[2] = 2 * G + atomicAdd((unsigned long long *)(flags + 10), 1ull);
             __syncthreads();
             STAMP(0);
 
@@ -487,8 +494,32 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             const uint64_t rem = geo.bits - tp * tile_bits;
             c.bt = rem < span ? (uint32_t)rem : span;
             const uint32_t bt = c.bt;
-            // the state entering tp (published one iteration ago)
-            if (j == 0) s_bc[0] = entering_state(lb, tp, flags);
+            // the state entering tp and its exclusive prefix: from the early
+            // snapshot, else by polling / the general look-back (wave 0)
+            if (j < 64) {
+                uint64_t excl = 0;
+                uint32_t sti = 0;
+#ifdef HH_STAMPS
+                const uint64_t q0 = __builtin_amdgcn_s_memtime();
+#endif
+                sti = entering_state(lb, tp, flags);
+                excl = tp > 0 ? lookback_excl(lb, tp, flags) : 0ull;
+#ifdef HH_STAMPS
+                COUNT(9, __builtin_amdgcn_s_memtime() - q0);
+                COUNT(10, 1);
+#endif
+                const uint64_t tab_w = s_tab[pb][hh_state_d(sti)];
+                if (j == 0) {
+                    st_sc1(&lb.inc[tp], hh_inc_pack(excl + (uint64_t)(int64_t)hh_tab_count(tab_w),
+                                                    hh_tab_state(tab_w)));
+                    s_bc[0] = sti;
+                    s_bc[1] = excl - (uint64_t)(int64_t)hh_state_delta(sti);
+                    if (lb.tdbg) {
+                        lb.tdbg[tp * 8 + 2] = excl;
+                        lb.tdbg[tp * 8 + 3] = tab_w;
+                    }
+                }
+            }
             __syncthreads();
             const uint32_t mem = s_mem[pb][j];
             const uint32_t st_in = (uint32_t)s_bc[0];
@@ -499,19 +530,6 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             if (live && j + rp.k < HH_NR) {
                 s_ein[j + rp.k] = (j + rp.k) * S + rp.e;
                 s_din[j + rp.k] = (int16_t)rp.delta;
-            }
-            if (j < 64) {
-                // output base: decoupled look-back over the predecessors
-                const uint64_t excl = tp > 0 ? lookback_excl(lb, tp, flags) : 0ull;
-                if (j == 0) {
-                    const uint64_t incl = excl + (uint64_t)(int64_t)hh_tab_count(tab_t);
-                    st_sc1(&lb.inc[tp], hh_inc_pack(incl, hh_tab_state(tab_t)));
-                    s_bc[1] = excl - (uint64_t)(int64_t)dprev;
-                    if (lb.tdbg) {
-                        lb.tdbg[tp * 8 + 2] = excl;
-                        lb.tdbg[tp * 8 + 3] = tab_t;
-                    }
-                }
             }
             __syncthreads();
             STAMP(4);
@@ -572,7 +590,11 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
         // the front half's tile becomes the pending one
         rp = rn;
         tp = front ? tn : ~0ull;
-        tn = front ? tn + G : tn;
+        if (front) {
+            tn = tq;
+            __syncthreads();                    // s_bc[2] (claimed by lane 0) visible
+            tq = tq < geo.ntiles ? s_bc[2] : tq;
+        }
         par ^= 1u;
     }
     STAMP_FLUSH(dbg);

@@ -27,4 +27,7 @@ print(f"ms={st['ms_total']:.3f} blocks={len(cyc)} ok={n == syn.decoded_bytes and
 tot = cyc.sum(0)
 for i, nm in enumerate(NAMES):
     print(f"  {nm:12s} {tot[i] / tot.sum() * 100:6.2f}%  mean/block {cyc[:, i].mean() / 2.4e6:8.3f} ms@2.4GHz")
+ex = raw[:, 8:12].astype(np.float64).sum(0)
+if ex[2]:
+    print(f"  look-backs {ex[2]:.0f} (entering state + exclusive prefix) at {ex[1] / ex[2]:.0f} cyc each")
 print(f"  total cycles/block mean {cyc.sum(1).mean():.3e} max {cyc.sum(1).max():.3e}")
