@@ -261,11 +261,12 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
                                uint32_t *mask = nullptr) {
     hh_cur u = hh_cur_at(c, p0);
     uint32_t n = 0;
-    /* boundary mask of the chain (bit i of tile word g <=> a symbol starts
-     * at 32 g + i), stored in the same transposed layout as the words; the
-     * region starts word-aligned.  (mlo, mhi) accumulate the words p>>5 and
-     * p>>5 + 1; am is the LDS index of word p>>5. */
-    uint32_t mlo = 0, mhi = 0, am = hh_idx(c, p0 >> 5);
+    /* Boundary mask of the chain: bit i of mask word g <=> a symbol starts
+     * at 32 g + i.  Word g is kept at LDS index hh_idx(g + 2) -- the index
+     * the cursor already holds (u.a) while it is in word g -- so recording
+     * costs no address arithmetic.  (mlo, mhi) accumulate words p>>5 and
+     * p>>5 + 1; the region starts word-aligned. */
+    uint32_t mlo = 0, mhi = 0;
     /* main loop: every symbol of a step starts before lim */
     const uint32_t lf = lim > c->maxadv ? lim - c->maxadv : 0u;
     while (u.p < lf) {
@@ -280,14 +281,13 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
         }
         n += ns;
         if (mask) {
-            const uint64_t m = (uint64_t)bm << (u.p & 31);
-            mlo |= (uint32_t)m;
-            mhi |= (uint32_t)(m >> 32);
-            mask[am] = mlo;
+            const uint64_t b = (uint64_t)bm << (u.p & 31);
+            mlo |= (uint32_t)b;
+            mhi |= (uint32_t)(b >> 32);
+            mask[u.a] = mlo;
             const bool cross = ((u.p + nb) >> 5) != (u.p >> 5);
             mlo = cross ? mhi : mlo;
             mhi = cross ? 0u : mhi;
-            am = cross ? hh_idx_next(c, am) : am;
         }
         hh_cur_adv(c, u, nb);
     }
@@ -297,19 +297,18 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
         const uint32_t o = hh_first_ge(L, lim - u.p);
         n += hh_syms_before(L, o);
         if (mask) {
-            const uint64_t m = (uint64_t)(L.bm & hh_lowmask(o)) << (u.p & 31);
-            mlo |= (uint32_t)m;
-            mhi |= (uint32_t)(m >> 32);
-            mask[am] = mlo;
+            const uint64_t b = (uint64_t)(L.bm & hh_lowmask(o)) << (u.p & 31);
+            mlo |= (uint32_t)b;
+            mhi |= (uint32_t)(b >> 32);
+            mask[u.a] = mlo;
             const bool cross = ((u.p + o) >> 5) != (u.p >> 5);
             mlo = cross ? mhi : mlo;
             mhi = cross ? 0u : mhi;
-            am = cross ? hh_idx_next(c, am) : am;
         }
         hh_cur_adv(c, u, o);
     }
     /* the word the chain stopped in, if it is still inside the region */
-    if (mask && (u.p >> 5) < (p0 >> 5) + c->sw) mask[am] = mlo;
+    if (mask && (u.p >> 5) < (p0 >> 5) + c->sw) mask[u.a] = mlo;
     *count = n;
     return u.p < c->bt ? u.p : c->bt;
 }
@@ -317,7 +316,7 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
 /* Symbols of a region's own chain that start before region offset off
  * (popcount of its mask below off). */
 HH_HD uint32_t hh_mask_rank(const hh_ctx *c, const uint32_t *mask, uint32_t R, uint32_t off) {
-    uint32_t cnt = 0, a = hh_idx(c, R >> 5);
+    uint32_t cnt = 0, a = hh_idx(c, (R >> 5) + 2);
     for (uint32_t w = 0; w < (off >> 5); w++) {
         cnt += hh_popc(mask[a]);
         a = hh_idx_next(c, a);
@@ -366,7 +365,7 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
             for (; A < Ec && it < HH_WALK_MAX; it++) {
                 hh_look L = hh_lookup(c, A);
                 const uint32_t off = A - R;
-                const uint32_t a0 = hh_idx(c, (R >> 5) + (off >> 5));
+                const uint32_t a0 = hh_idx(c, (R >> 5) + (off >> 5) + 2);   /* mask word */
                 const uint32_t m = hh_funnel(mask[hh_idx_next(c, a0)], mask[a0], off & 31);
                 const uint32_t hit = L.bm & m & hh_lowmask(Ec - A);
                 if (hit) {

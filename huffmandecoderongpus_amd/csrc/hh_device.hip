@@ -346,6 +346,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     __shared__ uint8_t s_mem[2][HH_NL];        // live masks over entering d (per pending tile)
     __shared__ uint8_t s_k[HH_NL];
     __shared__ int32_t s_part[HH_NL / 64][HH_KM];
+    __shared__ int32_t s_cd[HH_KM];            // per-d counts of the partially live lanes
     __shared__ uint32_t s_ost[HH_KM];
     __shared__ uint64_t s_tab[2][HH_KM];       // transfer table (per pending tile)
     __shared__ int32_t s_tmp[HH_NL / 64];
@@ -443,6 +444,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
 
             // transfer table: live masks (exceptions, ascending, by one lane),
             // charged count and leaving state for every entering d
+            if (j < HH_KM) s_cd[j] = 0;
             const uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt);   // barriers inside
             if (j == 0) {
                 for (uint32_t i = 0; i < nexc; i++) {
@@ -460,16 +462,21 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 for (uint32_t d = 0; d < HH_KM; d++)
                     if ((mem >> d) & 1u) s_ost[d] = os;
             }
+            // lanes live for every entering d: one block sum; the few others
+            // (lanes < HH_KM, covered lanes): per-d LDS atomics
+            const uint32_t full = (1u << HH_KM) - 1u;
+            const int32_t v = wave_sum(mem == full ? charged : 0);
+            if ((j & 63u) == 0) s_part[j >> 6][0] = v;
+            if (mem != full) {
 #pragma unroll
-            for (uint32_t d = 0; d < HH_KM; d++) {
-                const int32_t v = wave_sum(((mem >> d) & 1u) ? charged : 0);
-                if ((j & 63u) == 0) s_part[j >> 6][d] = v;
+                for (uint32_t d = 0; d < HH_KM; d++)
+                    if ((mem >> d) & 1u) atomicAdd(&s_cd[d], charged);
             }
             __syncthreads();
             if (j < HH_KM) {
-                int32_t cnt = 0;
+                int32_t cnt = s_cd[j];
 #pragma unroll
-                for (uint32_t w = 0; w < HH_NL / 64; w++) cnt += s_part[w][j];
+                for (uint32_t w = 0; w < HH_NL / 64; w++) cnt += s_part[w][0];
                 const uint64_t row = hh_tab_pack(cnt, s_ost[j]);
                 s_tab[par][j] = row;
                 if (j > 0) st_sc1(&lb.tabs[tn * HH_KM + j], HH_AGG | row);
