@@ -355,6 +355,9 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
     uint32_t A = x < bt ? x : bt;
     int32_t ca = 0;
     uint32_t it = 0;
+    hh_cur u = {0u, 0u, 0u, 0u, 0u};
+    uint32_t ml = 0, mh = 0;
+    bool cur_ok = false;
     for (uint32_t k = 1; k <= HH_KM; k++) {
         const uint32_t rg = j + k;
         const uint32_t R = rg * S;
@@ -362,31 +365,48 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
         const int32_t ca0 = ca;
         const uint32_t e = A > R ? A - R : 0u;   /* A == bt <= R: stream ended */
         if (mask && rg < nmask) {
-            for (; A < Ec && it < HH_WALK_MAX; it++) {
-                hh_look L = hh_lookup(c, A);
-                const uint32_t off = A - R;
-                const uint32_t a0 = hh_idx(c, (R >> 5) + (off >> 5) + 2);   /* mask word */
-                const uint32_t m = hh_funnel(mask[hh_idx_next(c, a0)], mask[a0], off & 31);
-                const uint32_t hit = L.bm & m & hh_lowmask(Ec - A);
+            /* chain cursor, with the mask words p>>5 and p>>5 + 1 (at LDS
+             * indices u.a and the next, see hh_region_count) in registers */
+            if (!cur_ok) {
+                u = hh_cur_at(c, A);
+                ml = mask[u.a];
+                mh = mask[hh_idx_next(c, u.a)];
+                cur_ok = true;
+            }
+            for (; u.p < Ec && it < HH_WALK_MAX; it++) {
+                const uint32_t win = hh_cur_win(u);
+                const uint32_t m = c->l1m[win & (HH_L1_SIZE - 1u)];
+                uint32_t lns = HH_M_NSYM(m), lnb = HH_M_NBITS(m), lbm = HH_M_BMASK(m);
+                if (lns == 0) {
+                    uint32_t sy;
+                    lnb = hh_escape(c, u.p, win, &sy);
+                    lns = 1;
+                    lbm = 1;
+                }
+                const uint32_t hit = lbm & hh_funnel(mh, ml, u.p & 31) & hh_lowmask(Ec - u.p);
                 if (hit) {
                     const uint32_t t = hh_ctz(hit);
-                    ca += (int32_t)hh_popc(L.bm & hh_lowmask(t));
+                    ca += (int32_t)hh_popc(lbm & hh_lowmask(t));
                     r.k = k;
                     r.e = e;
                     r.cov = (uint32_t)ca0;
-                    r.delta = (ca - ca0) - (int32_t)hh_mask_rank(c, mask, R, off + t);
+                    r.delta = (ca - ca0) - (int32_t)hh_mask_rank(c, mask, R, u.p - R + t);
                     return r;
                 }
-                if (A + L.nb <= Ec) {
-                    A += L.nb;
-                    ca += (int32_t)L.ns;
+                uint32_t adv = lnb;
+                if (u.p + lnb <= Ec) {
+                    ca += (int32_t)lns;
                 } else {
-                    const uint32_t o = hh_first_ge(L, Ec - A);
-                    ca += (int32_t)hh_syms_before(L, o);
-                    A += o;
+                    adv = lbm & ~hh_lowmask(Ec - u.p) ? hh_ctz(lbm & ~hh_lowmask(Ec - u.p)) : lnb;
+                    ca += (int32_t)hh_popc(lbm & hh_lowmask(adv));
                 }
+                const bool cross = ((u.p + adv) >> 5) != (u.p >> 5);
+                hh_cur_adv(c, u, adv);
+                const uint32_t nm = mask[hh_idx_next(c, u.a)];
+                ml = cross ? mh : ml;
+                mh = cross ? nm : mh;
             }
-            if (A > bt) A = bt;
+            A = u.p < bt ? u.p : bt;
             const uint32_t xr = xs[rg] < bt ? xs[rg] : bt;
             if (A == xr) {                  /* merged at the region's exit */
                 r.k = k;

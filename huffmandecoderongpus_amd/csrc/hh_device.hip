@@ -445,6 +445,10 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             // transfer table: live masks (exceptions, ascending, by one lane),
             // charged count and leaving state for every entering d
             if (j < HH_KM) s_cd[j] = 0;
+#ifdef HH_STAMPS
+            __syncthreads();
+            STAMP(7);
+#endif
             const uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt);   // barriers inside
             if (j == 0) {
                 for (uint32_t i = 0; i < nexc; i++) {

@@ -11,7 +11,7 @@ import torch  # noqa: E402
 import huffmandecoderongpus_amd as H  # noqa: E402
 from huffmandecoderongpus_amd import synth  # noqa: E402
 
-NAMES = ["stage", "pass1", "walks", "table", "entry+lookback", "scan", "pass2"]
+NAMES = ["stage", "pass1", "walks", "table", "entry+lookback", "scan", "pass2", "walk-wait"]
 size = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 hf, text = synth.load_source(os.path.join(ROOT, "files"))
 syn = synth.tiled_stream(hf, text, size << 20)
