@@ -66,6 +66,16 @@ class _Stats(C.Structure):
                 ("repairs", C.c_uint64), ("exact_fallback", C.c_int)]
 
 
+class _Range(C.Structure):
+    _fields_ = [("bits_avail", C.c_uint64), ("ntiles", C.c_uint64), ("prologue", C.c_uint64),
+                ("in_state", C.c_uint32)]
+
+
+class _RangeOut(C.Structure):
+    _fields_ = [("out_len", C.c_uint64), ("leave_state", C.c_uint32), ("const_seen", C.c_uint32),
+                ("entry_state", C.c_uint32), ("entry_exact", C.c_uint32)]
+
+
 FLAG_FORCE_EXACT = 1
 _lib_handle: Optional[C.CDLL] = None
 
@@ -87,6 +97,9 @@ _SIGS = {
     "hh_decoder_stats": ([C.c_void_p, C.POINTER(_Stats)], C.c_int),
     "hh_decode_device": ([C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                           C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
+    "hh_decoder_tile_bits": ([C.c_void_p, C.POINTER(C.c_uint64)], C.c_int),
+    "hh_decode_device_range": ([C.c_void_p, C.c_void_p, C.POINTER(_Range), C.c_void_p,
+                                C.c_uint64, C.POINTER(_RangeOut), C.c_void_p], C.c_int),
     "hh_decode_host": ([C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                         C.POINTER(C.c_uint64)], C.c_int),
     "hh_stage_initbitsindex": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p], C.c_int),
@@ -271,6 +284,25 @@ class Decoder:
         s = stream if stream is not None else torch.cuda.current_stream(data.device)
         return self.decode_device_ptr(data.data_ptr(), bits, out.data_ptr(), out.numel(),
                                       s.cuda_stream)
+
+    def tile_bits(self) -> int:
+        """Bits per tile for the current tree (segments are whole tiles)."""
+        tb = C.c_uint64(0)
+        _check(lib().hh_decoder_tile_bits(self._h, C.byref(tb)), "tile_bits")
+        return int(tb.value)
+
+    def decode_range_ptr(self, d_data: int, bits_avail: int, ntiles: int, in_state: int,
+                         d_out: int, cap: int, stream: int = 0, prologue: int = 0) -> dict:
+        """One segment (hh_decode_device_range): tiles [0, ntiles) of the
+        bits at d_data, entered in state in_state; the first `prologue`
+        tiles only locate the entry of tile `prologue`."""
+        rg = _Range(bits_avail, ntiles, prologue, in_state)
+        ro = _RangeOut()
+        _check(lib().hh_decode_device_range(self._h, d_data, C.byref(rg), d_out, cap,
+                                            C.byref(ro), stream or None), "decode_range")
+        return {"out_len": int(ro.out_len), "leave_state": int(ro.leave_state),
+                "const_seen": bool(ro.const_seen), "entry_state": int(ro.entry_state),
+                "entry_exact": bool(ro.entry_exact)}
 
     def stage_pipeline_ptr(self, d_data: int, bits: int, d_out: int, cap: int,
                            stream: int = 0) -> int:

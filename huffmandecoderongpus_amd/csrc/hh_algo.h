@@ -519,6 +519,9 @@ HH_HD uint64_t hh_inc_pack(uint64_t prefix, uint32_t state) {
     return HH_INC | (prefix & HH_INC_MASK) | ((uint64_t)state << 40);
 }
 HH_HD uint32_t hh_inc_state(uint64_t g) { return (uint32_t)(g >> 40) & 0x1fffffu; }
+/* the prefix, sign-extended (a segment's virtual predecessor carries the
+ * entry correction, which may be negative) */
+HH_HD uint64_t hh_inc_prefix(uint64_t g) { return (uint64_t)((int64_t)(g << 24) >> 24); }
 
 /* Region size for a code whose lengths are all multiples of g: a multiple
  * of 32 (whole words per region column) and of g (region starts on the

@@ -149,8 +149,8 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // aggregate when that is CONST (the common case: available as soon as t-1's
 // walks are done), else from its inclusive granule (t-1 resolved its own
 // entering state first).
-__device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t *flags) {
-    if (t == 0) return hh_state_pack(0, 0, 0);
+__device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t in_state, uint32_t *flags) {
+    if (t == 0) return in_state;
     const uint64_t g = poll_granule(&lb.agg[t - 1], flags);
     if (g & HH_CST) return hh_tab_state(g);
     return hh_inc_state(poll_granule(&lb.inc[t - 1], flags));
@@ -164,11 +164,15 @@ __device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t *fla
 // granule appears closer); row 0 is u's aggregate, rows d > 0 are granules
 // of their own.
 #define HH_LBV 8   // tiles per lane per look-back round (512-tile window)
-__device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flags) {
+__device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t in_state, uint64_t emit_from,
+                                  uint32_t *flags) {
     constexpr uint32_t V = HH_LBV;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t st0 = HH_AGG | HH_CST | hh_tab_pack(0, hh_state_pack(0, 0, 0));
-    const uint64_t in0 = hh_inc_pack(0, hh_state_pack(0, 0, 0));
+    // tile -1: a CONST aggregate leaving in_state; its inclusive value is
+    // the entry correction (so that tile 0's output base is 0), unless a
+    // prologue carries it (see the table rows of prologue tiles)
+    const uint64_t st0 = HH_AGG | HH_CST | hh_tab_pack(0, in_state);
+    const uint64_t in0 = hh_inc_pack(emit_from ? 0ull : (uint64_t)(int64_t)hh_state_delta(in_state), in_state);
     uint64_t excl = 0;
     int64_t top = (int64_t)t - 1;
     uint32_t rounds = 0;
@@ -229,7 +233,7 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t *flag
         excl += wave_sum64((uint64_t)csum);
         rounds++;
         if (ofirst < 64u * V) {
-            const uint64_t pre = incv & HH_INC_MASK;
+            const uint64_t pre = hh_inc_prefix(incv);
             if (lb.tdbg && lane == 0) {
                 lb.tdbg[t * 8 + 4] = (uint64_t)(top - (int64_t)ofirst);
                 lb.tdbg[t * 8 + 5] = pre;
@@ -324,6 +328,9 @@ struct Geometry {
     uint32_t S, sw, magic;
     uint32_t vec4;       // 16-B aligned payload and sw % 4 == 0
     uint32_t maxadv;     // max(HH_P, longest code)
+    uint32_t in_state;   // state entering tile 0 (a shard's entry; 0 at the stream start)
+    uint64_t emit_from;  // tiles before this one are a prologue: decoded for their
+                         // leaving state only (a shard's probe of its predecessor)
 };
 
 // Per-lane results of a tile's front half, kept in registers until its back
@@ -481,6 +488,9 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 int32_t cnt = s_cd[j];
 #pragma unroll
                 for (uint32_t w = 0; w < HH_NL / 64; w++) cnt += s_part[w][0];
+                // a prologue tile emits nothing; the last one charges the
+                // entry correction of the first emitted tile instead
+                if (tn < geo.emit_from) cnt = tn + 1 == geo.emit_from ? hh_state_delta(s_ost[j]) : 0;
                 const uint64_t row = hh_tab_pack(cnt, s_ost[j]);
                 s_tab[par][j] = row;
                 if (j > 0) st_sc1(&lb.tabs[tn * HH_KM + j], HH_AGG | row);
@@ -493,6 +503,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 for (uint32_t d = 1; d < HH_KM; d++)
                     cst = cst && hh_tab_state(s_tab[par][d]) == hh_tab_state(s_tab[par][0]);
                 st_sc1(&lb.agg[tn], HH_AGG | (cst ? HH_CST : 0ull) | s_tab[par][0]);
+                if (cst && flags[tn < geo.emit_from ? 12 : 13] == 0u) flags[tn < geo.emit_from ? 12 : 13] = 1u;
             }
             rn.n = n; rn.k = kk; rn.e = wk.e; rn.cov = wk.cov; rn.delta = wk.delta;
             STAMP(3);
@@ -505,16 +516,15 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             const uint64_t rem = geo.bits - tp * tile_bits;
             c.bt = rem < span ? (uint32_t)rem : span;
             const uint32_t bt = c.bt;
-            // the state entering tp and its exclusive prefix: from the early
-            // snapshot, else by polling / the general look-back (wave 0)
+            // the state entering tp (from tp-1's aggregate, or its inclusive
+            // granule) and tp's exclusive prefix (decoupled look-back), wave 0
             if (j < 64) {
-                uint64_t excl = 0;
-                uint32_t sti = 0;
 #ifdef HH_STAMPS
                 const uint64_t q0 = __builtin_amdgcn_s_memtime();
 #endif
-                sti = entering_state(lb, tp, flags);
-                excl = tp > 0 ? lookback_excl(lb, tp, flags) : 0ull;
+                const uint32_t sti = entering_state(lb, tp, geo.in_state, flags);
+                const uint64_t excl = tp > 0 ? lookback_excl(lb, tp, geo.in_state, geo.emit_from, flags)
+                                             : (geo.emit_from ? 0ull : (uint64_t)(int64_t)hh_state_delta(geo.in_state));
 #ifdef HH_STAMPS
                 COUNT(9, __builtin_amdgcn_s_memtime() - q0);
                 COUNT(10, 1);
@@ -524,7 +534,9 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                     st_sc1(&lb.inc[tp], hh_inc_pack(excl + (uint64_t)(int64_t)hh_tab_count(tab_w),
                                                     hh_tab_state(tab_w)));
                     s_bc[0] = sti;
-                    s_bc[1] = excl - (uint64_t)(int64_t)hh_state_delta(sti);
+                    s_bc[1] = excl - (uint64_t)(int64_t)hh_state_delta(sti);   // output base
+                    if (tp == geo.ntiles - 1) flags[14] = hh_tab_state(tab_w);
+                    if (tp == geo.emit_from) flags[15] = sti;
                     if (lb.tdbg) {
                         lb.tdbg[tp * 8 + 2] = excl;
                         lb.tdbg[tp * 8 + 3] = tab_w;
@@ -546,7 +558,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             STAMP(4);
             const uint32_t e_in = j == d_t ? d_t * S + hh_state_e(st_in) : s_ein[j];
             const int32_t d_in = j == d_t ? dprev : (int32_t)s_din[j];
-            const uint32_t rc = live ? (uint32_t)((int32_t)(rp.n + rp.cov) + d_in) : 0u;
+            const uint32_t rc = live && tp >= geo.emit_from ? (uint32_t)((int32_t)(rp.n + rp.cov) + d_in) : 0u;
             int32_t Tout_i;
             const uint32_t L = (uint32_t)block_excl_scan((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
             const uint32_t Tout = (uint32_t)Tout_i;
@@ -557,7 +569,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                     flags[2] = (uint32_t)tot;
                     flags[3] = (uint32_t)(tot >> 32);
                 }
-                if (P0 + Tout > cap) atomicOr(flags, (uint32_t)F_OVER);
+                if (tp >= geo.emit_from && P0 + Tout > cap) atomicOr(flags, (uint32_t)F_OVER);
                 if (lb.tdbg) {
                     lb.tdbg[tp * 8 + 0] = P0;
                     lb.tdbg[tp * 8 + 1] = Tout | ((uint64_t)st_in << 32);
@@ -570,7 +582,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             // dwords, then the ragged end
             hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
             const uint32_t y = (j + rp.k) * S + rp.e;
-            const uint32_t pe = (live && P0 + Tout <= cap) ? (y < bt ? y : bt) : 0u;
+            const uint32_t pe = (live && tp >= geo.emit_from && P0 + Tout <= cap) ? (y < bt ? y : bt) : 0u;
             if (cu.p < pe) {
                 uint8_t *ob = out + P0;
                 uint32_t o = L, val, k;
@@ -879,31 +891,24 @@ static int size_grid(hh_decoder *d, size_t lds, kdec_t kf) {
     return HH_OK;
 }
 
-extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits, void *d_out,
-                                uint64_t cap, uint64_t *out_len, void *hip_stream) {
-    if (!d || !out_len || (!d_data && bits) || (!d_out && cap)) return HH_ERR_ARG;
-    if (!d->have_tree) return HH_ERR_ARG;
-    if (((uintptr_t)d_data & 3u) != 0) return HH_ERR_ARG;   // word loads
-    // NULL is the default stream (ordered with the caller's default-stream
-    // work, e.g. torch's), never the decoder's private non-blocking stream
-    hipStream_t st = (hipStream_t)hip_stream;
-    HIP_OK(hipSetDevice(d->device));
-    memset(&d->stats, 0, sizeof(d->stats));
-    *out_len = 0;
-    if (bits == 0) return HH_OK;
-    if (!fast_path_ok(d)) {
-        d->stats.exact_fallback = 1;
-        return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
-    }
+// The fused decode of tiles [0, ntiles) of the segment at d_data
+// (bits_avail readable stream bits), entered at in_state.
+static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, uint64_t ntiles,
+                       uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
+                       hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *cst_pro,
+                       uint32_t *cst_seg, uint32_t *entry) {
     Geometry geo;
-    geo.bits = bits;
+    geo.bits = bits_avail;
     geo.S = d->S;
     geo.sw = d->S / 32;
     geo.magic = hh_magic(geo.sw);
     geo.maxadv = d->ht->maxlen > HH_P ? (uint32_t)d->ht->maxlen : HH_P;
-    geo.nwords = ((bits + 7) / 8 + HH_PAYLOAD_PAD) / 4;
+    geo.nwords = ((bits_avail + 7) / 8 + HH_PAYLOAD_PAD) / 4;
+    geo.in_state = in_state;
+    geo.emit_from = emit_from;
     const uint64_t tb = (uint64_t)HH_NR * d->S;
-    geo.ntiles = (bits + tb - 1) / tb;
+    const uint64_t all = (bits_avail + tb - 1) / tb;
+    geo.ntiles = ntiles && ntiles < all ? ntiles : all;
     geo.vec4 = (((uintptr_t)d_data & 15u) == 0) && (geo.sw % 4 == 0);
     // workspace: [flags 64 B | agg[ntiles] | inc[ntiles] | tabs[ntiles][KM]] (zeroed)
     //            | (HH_DEBUG_TILES) tdbg[ntiles][8]
@@ -932,27 +937,85 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
                        d->tab, lb, (uint8_t *)d_out, cap, d_flags, d->d_dbg);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d->ev[1], st));
-    HIP_OK(hipMemcpyAsync(d->h_flags, d_flags, 16, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(d->h_flags, d_flags, 64, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     const uint32_t fl = d->h_flags[0];
-    const uint64_t total = (uint64_t)d->h_flags[2] | ((uint64_t)d->h_flags[3] << 32);
+    *total = (uint64_t)d->h_flags[2] | ((uint64_t)d->h_flags[3] << 32);
+    *leave = d->h_flags[14];
+    *cst_pro = d->h_flags[12];
+    *cst_seg = d->h_flags[13];
+    *entry = emit_from < geo.ntiles ? d->h_flags[15] : in_state;
+    if (emit_from >= geo.ntiles) *total = 0;
     float ms = 0;
     hipEventElapsedTime(&ms, d->ev[0], d->ev[1]);
     d->stats.ms_total = ms;
     d->stats.ms_emit = ms;
     d->stats.lanes = geo.ntiles * HH_NR;
-    d->stats.out_len = total;
+    d->stats.out_len = *total;
     if (fl & F_TIMEOUT) return HH_ERR_TIMEOUT;
-    if (fl & F_FAIL) {
-        // A walk found no shared boundary inside the next region (a code that
-        // does not resynchronise within S bits): take the exact path.
+    if (fl & F_FAIL) return HH_ERR_UNSUPPORTED;
+    if (*total > cap || (fl & F_OVER)) return HH_ERR_CAPACITY;
+    return HH_OK;
+}
+
+extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits, void *d_out,
+                                uint64_t cap, uint64_t *out_len, void *hip_stream) {
+    if (!d || !out_len || (!d_data && bits) || (!d_out && cap)) return HH_ERR_ARG;
+    if (!d->have_tree) return HH_ERR_ARG;
+    if (((uintptr_t)d_data & 3u) != 0) return HH_ERR_ARG;   // word loads
+    // NULL is the default stream (ordered with the caller's default-stream
+    // work, e.g. torch's), never the decoder's private non-blocking stream
+    hipStream_t st = (hipStream_t)hip_stream;
+    HIP_OK(hipSetDevice(d->device));
+    memset(&d->stats, 0, sizeof(d->stats));
+    *out_len = 0;
+    if (bits == 0) return HH_OK;
+    if (!fast_path_ok(d)) {
+        d->stats.exact_fallback = 1;
+        return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
+    }
+    uint64_t total = 0;
+    uint32_t leave = 0, cp = 0, cs = 0, en = 0;
+    int rc = decode_fast(d, d_data, bits, 0, hh_state_pack(0, 0, 0), 0, d_out, cap, st, &total,
+                         &leave, &cp, &cs, &en);
+    if (rc == HH_ERR_UNSUPPORTED) {
+        // A walk found no shared boundary within HH_KM regions (a code that
+        // does not resynchronise): take the exact path.
         d->stats.exact_fallback = 1;
         d->stats.repairs = 1;
         return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
     }
     *out_len = total;
-    if (total > cap || (fl & F_OVER)) return HH_ERR_CAPACITY;
+    return rc;
+}
+
+extern "C" int hh_decoder_tile_bits(const hh_decoder *d, uint64_t *tile_bits) {
+    if (!d || !tile_bits || !d->have_tree) return HH_ERR_ARG;
+    *tile_bits = (uint64_t)HH_NR * d->S;
     return HH_OK;
+}
+
+extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const hh_range *rg,
+                                      void *d_out, uint64_t cap, hh_range_out *ro,
+                                      void *hip_stream) {
+    if (!d || !rg || !ro || (!d_data && rg->bits_avail) || (!d_out && cap)) return HH_ERR_ARG;
+    if (!d->have_tree) return HH_ERR_ARG;
+    if (((uintptr_t)d_data & 3u) != 0) return HH_ERR_ARG;
+    hipStream_t st = (hipStream_t)hip_stream;
+    HIP_OK(hipSetDevice(d->device));
+    memset(&d->stats, 0, sizeof(d->stats));
+    memset(ro, 0, sizeof(*ro));
+    ro->leave_state = ro->entry_state = rg->in_state;
+    if (rg->bits_avail == 0) return HH_OK;
+    // segments need the fused path (tile tables, entry states); a tree it
+    // does not support is decoded whole, unsharded
+    if (!fast_path_ok(d) || hh_state_d(rg->in_state) >= HH_KM) return HH_ERR_UNSUPPORTED;
+    uint32_t cp = 0;
+    const int rc = decode_fast(d, d_data, rg->bits_avail, rg->ntiles, rg->in_state, rg->prologue,
+                               d_out, cap, st, &ro->out_len, &ro->leave_state, &cp,
+                               &ro->const_seen, &ro->entry_state);
+    ro->entry_exact = rg->prologue == 0 || cp != 0;
+    return rc;
 }
 
 extern "C" int hh_decode_host(hh_decoder *d, const uint8_t *data, uint64_t bits, uint8_t *out,

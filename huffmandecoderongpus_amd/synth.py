@@ -74,19 +74,30 @@ def load_source(files_dir: str, name: str = "kjv.txt", device: int = 0, check_sh
     return hf, text
 
 
+def cut_bits(hf, text: np.ndarray, target_bytes: int) -> tuple[int, int]:
+    """(bits, symbols) of the tiled stream cut at the last whole symbol that
+    fits target_bytes of payload (what tiled_stream(..., bit_offset=0) makes)."""
+    B0 = hf.bits
+    bounds = np.concatenate([[0], np.cumsum(code_lengths(hf.tree())[text])])
+    c, within = divmod(8 * target_bytes, B0)
+    k = int(np.searchsorted(bounds, within, side="right")) - 1
+    return c * B0 + int(bounds[k]), c * len(text) + k
+
+
 def tiled_stream(hf, text: np.ndarray, target_bytes: int, device="cuda",
-                 bit_offset: int = 0, halo_bytes: int = 0) -> Synthetic:
+                 bit_offset: int = 0, halo_bytes: int = 0, bits: int | None = None) -> Synthetic:
     """Bits [bit_offset, bit_offset + 8*target_bytes) of the infinite tiling of
-    hf's payload, cut at the last whole symbol; plus halo_bytes more payload
-    bytes after it (for a shard's successor walk).  bit_offset must be a
-    multiple of 32 and a code boundary is not required there."""
+    hf's payload, cut at the last whole symbol (or, with `bits`, exactly that
+    many bits, no cut); plus halo_bytes more payload bytes after it (for a
+    shard's successor walk).  bit_offset must be a multiple of 32 and a code
+    boundary is not required there."""
     import torch
     B0 = hf.bits
     P = torch.from_numpy(hf.payload.copy()).to(device)
     lens = code_lengths(hf.tree())[text]
     bounds = np.concatenate([[0], np.cumsum(lens)])          # symbol starts + end
     assert bounds[-1] == B0
-    tgt_bits = 8 * target_bytes
+    tgt_bits = 8 * target_bytes if bits is None else bits
     gen_bits = tgt_bits + 8 * halo_bytes
     nbytes = (gen_bits + 7) // 8
     out = torch.zeros(nbytes + 64 + 8, dtype=torch.uint8, device=device)
@@ -114,7 +125,8 @@ def tiled_stream(hf, text: np.ndarray, target_bytes: int, device="cuda",
     within = end_global - cidx * B0
     k = int(np.searchsorted(bounds, within, side="right")) - 1   # boundaries <= within
     cut_global = cidx * B0 + int(bounds[k])
-    bits = cut_global - bit_offset
+    if bits is None:
+        bits = cut_global - bit_offset
     # symbols in the shard (only meaningful for bit_offset == 0)
     copies, tail = int(cidx), int(k)
     if halo_bytes == 0:

@@ -159,6 +159,53 @@ int hh_decode_device(hh_decoder *dec, const void *d_data, uint64_t bits,
                      void *d_out, uint64_t cap, uint64_t *out_len,
                      void *hip_stream);
 
+/* ---------------------------------------------------------------------- */
+/* Segments (multi-GPU shards).  The stream is cut into tiles of           */
+/* hh_decoder_tile_bits() bits; a segment is a run of whole tiles.  The    */
+/* chain enters a segment in a STATE (region, offset, count correction) */
+/* that is the state leaving the previous segment; the stream starts in   */
+/* state 0.  A segment's output is the symbols from its entry point up to */
+/* its successor's, i.e. the segments' outputs concatenate to the stream's */
+/* (the reference has no multi-device path).              */
+/* ---------------------------------------------------------------------- */
+int hh_decoder_tile_bits(const hh_decoder *dec, uint64_t *tile_bits);
+
+typedef struct {
+    uint64_t bits_avail;     /* readable stream bits at d_data: the segment's
+                                tiles plus at least one tile after them (the
+                                next segment's first regions), or up to the
+                                end of the stream for the last segment     */
+    uint64_t ntiles;         /* tiles to decode; 0 = all of bits_avail      */
+    uint64_t prologue;       /* the first `prologue` tiles are the end of   */
+                             /* the PREVIOUS segment: decoded only to find  */
+                             /* the state entering tile `prologue`, where   */
+                             /* output starts (0: start at tile 0)          */
+    uint32_t in_state;       /* state entering tile 0                       */
+} hh_range;
+
+typedef struct {
+    uint64_t out_len;        /* symbols written                             */
+    uint32_t leave_state;    /* state leaving the last tile                 */
+    uint32_t const_seen;     /* 1: some emitted tile's table is CONST, so   */
+                             /* leave_state does not depend on the entry    */
+    uint32_t entry_state;    /* state entering the first emitted tile       */
+    uint32_t entry_exact;    /* 1: the entry state of the first emitted     */
+                             /* tile is exact (no prologue, or some         */
+                             /* prologue tile's table is CONST)             */
+} hh_range_out;
+
+/* Decode a segment (device pointers, stream as hh_decode_device).  A
+ * shard that holds the last tiles of its predecessor before its own decodes
+ * them as a prologue (in_state 0) and so finds its own entry state locally
+ * (exact whenever one of those tiles is CONST, which real codes almost
+ * always are); hh_range_out lets the caller check the entries against the
+ * predecessors' leave_state and redo a segment entered wrongly.  Trees
+ * the fused path does not handle (codes longer than 32 bits, codes that
+ * never resynchronise) return HH_ERR_UNSUPPORTED: decode those whole. */
+int hh_decode_device_range(hh_decoder *dec, const void *d_data, const hh_range *rg,
+                           void *d_out, uint64_t cap, hh_range_out *out,
+                           void *hip_stream);
+
 /* Host-to-host convenience: H2D, hh_decode_device, D2H.  This is the scope
  * the reference times in evaluate() (decodeUtil.c:41-43). */
 int hh_decode_host(hh_decoder *dec, const uint8_t *data, uint64_t bits,

@@ -28,21 +28,30 @@ extern "C" {
 
 // stats[0]=tiles stats[1]=walks with k > 1 stats[2]=failed walks
 // stats[3]=region bits used stats[4]=max k stats[5]=non-CONST tiles
-int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *sym,
-                      int32_t nodes, const uint8_t *data, uint64_t bits, uint32_t S,
-                      uint8_t *out, uint64_t cap, int64_t *stats) {
+// stats[6]=CONST prologue tiles stats[7]=CONST emitted tiles
+// A segment: tiles [0, ntiles) (0 = all) of the bits at data, entered at
+// in_state; *leave receives the state leaving the last tile (the kernel's
+// hh_decode_device_range).
+int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uint8_t *sym,
+                            int32_t nodes, const uint8_t *data, uint64_t bits, uint32_t S,
+                            uint64_t ntiles_req, uint64_t prologue, uint32_t in_state,
+                            uint8_t *out, uint64_t cap, int64_t *stats, uint32_t *leave,
+                            uint32_t *entry) {
     hh_tree tree = {nodes, izero, ione, sym};
     static hh_tables T;   // large; not reentrant (test helper)
     int rc = hh_tables_build(&tree, &T);
     if (rc) return rc;
-    for (int i = 0; i < 6; i++) stats[i] = 0;
+    for (int i = 0; i < 8; i++) stats[i] = 0;
     if (S == 0) S = hh_pick_region_bits((uint32_t)T.len_gcd);
     stats[3] = S;
+    if (leave) *leave = in_state;
+    if (entry) *entry = in_state;
     if (bits == 0) return 0;
     if (S < 32 || S % 32 || S > 32 * HH_SW_MAX) return HH_ERR_ARG;
     const uint32_t sw = S / 32;
     const uint64_t TB = (uint64_t)HH_NR * S;
-    const uint64_t ntiles = (bits + TB - 1) / TB;
+    const uint64_t all = (bits + TB - 1) / TB;
+    const uint64_t ntiles = ntiles_req && ntiles_req < all ? ntiles_req : all;
     const uint64_t nbytes = (bits + 7) / 8;
     const uint32_t span = HH_NCOL * S;
     std::vector<uint32_t> w((size_t)sw * HH_NLS);
@@ -68,8 +77,10 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
     };
 
     uint64_t base = 0;                            // P_0 of the tile
-    int64_t excl = 0;                             // charged prefix of tiles < t
-    uint32_t st_in = hh_state_pack(0, 0, 0);      // resolved entering state
+    uint32_t st_in = in_state;                    // resolved entering state
+    // charged prefix of tiles < t, + the entry correction (carried by the
+    // last prologue tile's counts when there is a prologue)
+    int64_t excl = prologue ? 0 : hh_state_delta(in_state);
     for (uint64_t t = 0; t < ntiles; t++) {
         hh_ctx c;
         const uint64_t tw0 = t * TB / 32;
@@ -135,6 +146,14 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
             if (ost[d] != ost[0]) cst = false;
         }
         if (!cst) stats[5]++;
+        if (cst) stats[t < prologue ? 6 : 7]++;
+        if (t < prologue) {                               // prologue tile: state only
+            const uint32_t so = ost[hh_state_d(st_in)];
+            excl += t + 1 == prologue ? hh_state_delta(so) : 0;
+            st_in = so;
+            continue;
+        }
+        if (t == prologue && entry) *entry = st_in;
         // entering state -> live lanes, entries, run counts
         const uint32_t d_t = hh_state_d(st_in), e_t = hh_state_e(st_in);
         const int32_t dprev = hh_state_delta(st_in);
@@ -184,7 +203,15 @@ int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *
         base = o;
         st_in = so;
     }
+    if (leave) *leave = st_in;
     return (int64_t)base;
+}
+
+int64_t hh_emu_decode(const int32_t *izero, const int32_t *ione, const uint8_t *sym,
+                      int32_t nodes, const uint8_t *data, uint64_t bits, uint32_t S,
+                      uint8_t *out, uint64_t cap, int64_t *stats) {
+    return hh_emu_decode_range(izero, ione, sym, nodes, data, bits, S, 0, 0, hh_state_pack(0, 0, 0),
+                               out, cap, stats, nullptr, nullptr);
 }
 
 }  // extern "C"

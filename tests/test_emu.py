@@ -40,7 +40,7 @@ def run_emu(emu, izero, ione, sym, data, bits, S):
     d = np.zeros((bits + 7) // 8 + 64, np.uint8)
     d[: (bits + 7) // 8] = np.asarray(data, np.uint8)[: (bits + 7) // 8]
     out = np.zeros(bits + 16, np.uint8)
-    st = np.zeros(6, np.int64)
+    st = np.zeros(8, np.int64)
     n = emu.hh_emu_decode(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), d.ctypes.data,
                           bits, S, out.ctypes.data, len(out), st.ctypes.data)
     return n, out[: max(n, 0)], st

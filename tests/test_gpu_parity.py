@@ -201,3 +201,124 @@ def test_synthetic_full_size(hh, files_dir, mib):
         dec.close()
         del out
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("world,probe", [(3, 2), (5, 1), (4, 0)])
+def test_segments_concatenate(hh, files_dir, world, probe):
+    """hh_decode_device_range on one GPU, shards planned as bench.py --gpus N
+    plans them, each with `probe` predecessor tiles as a prologue; every
+    "rank" is a thread running shard.settle over an in-process gather (one
+    decoder, calls serialised).  probe 0: entries are guesses that the
+    exchange must catch.  The outputs must concatenate to the oracle's."""
+    import threading
+    import torch
+    from huffmandecoderongpus_amd import shard
+    path = os.path.join(files_dir, "kjv.txt.huff")
+    hf = hh.HuffFile.load(path)
+    ref = O.OracleHuff.load(path).chain_decode()
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(hf.tree())
+        tb = dec.tile_bits()
+        pay = torch.zeros(len(hf.payload) + 256, dtype=torch.uint8, device="cuda")
+        pay[:len(hf.payload)] = torch.from_numpy(hf.payload.copy()).cuda()
+        segs = [shard.plan(hf.bits, tb, world, r, probe) for r in range(world)]
+        outs = [torch.zeros(hf.bits + 64, dtype=torch.uint8, device="cuda") for _ in segs]
+        lock = threading.Lock()
+        bar = threading.Barrier(world)
+        slots = [None] * world
+        final = [None] * world
+        redone = [0] * world
+
+        def run(r, in_state, prologue):
+            s = segs[r]
+            skip = s.prologue - prologue
+            with lock:
+                res = dec.decode_range_ptr(pay.data_ptr() + (s.buf_bit + skip * tb) // 8,
+                                           s.bits_avail - skip * tb, s.ntiles - skip, in_state,
+                                           outs[r].data_ptr(), outs[r].numel(), 0,
+                                           prologue=prologue)
+                torch.cuda.synchronize()
+            res["in_state"] = res["entry_state"]
+            return res
+
+        def rank_main(r):
+            def gather(vals):
+                slots[r] = list(vals)
+                bar.wait()
+                rows = [list(x) for x in slots]
+                bar.wait()
+                return rows
+
+            def redo(st):
+                redone[r] += 1
+                return run(r, st, 0)
+
+            first = run(r, 0, segs[r].prologue)
+            if segs[r].prologue == 0 and segs[r].t0 > 0:
+                first["entry_exact"] = False
+            final[r] = shard.settle(first, redo, gather, r, world)[0]
+
+        th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        got = torch.cat([outs[r][:final[r]["out_len"]] for r in range(world)]).cpu().numpy()
+        assert len(got) == len(ref) and np.array_equal(got, ref)
+        if probe:
+            assert sum(redone) == 0
+        else:
+            assert sum(redone) >= 1
+    finally:
+        dec.close()
+
+
+def _shard_rank(rank, world, port, mib, q):
+    import torch
+    import torch.distributed as dist
+    import huffmandecoderongpus_amd as H
+    from huffmandecoderongpus_amd import shard, synth
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}",
+                                rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        hf, text = synth.load_source(os.path.join(ROOT, "files"))
+        job = shard.ShardJob(hf, text, mib << 20, rank, world, 0)
+        ok = True
+        for _ in range(2):
+            job.decode_step()
+            torch.cuda.synchronize()
+            ok = ok and job.verify()
+        q.put((rank, ok, job.decoded_bytes, job.seg.prologue))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, repr(e), 0, 0))
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_shard_job_two_ranks_one_gpu():
+    """bench.py's multi-GPU path (ShardJob: shard plan, prologue entry,
+    settle exchange, per-rank verification against the tiled text) with two
+    processes sharing GPU 0 over gloo (RCCL needs distinct GPUs)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_shard_rank, args=(r, 2, port, 32, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    for rank, ok, n, pro in got:
+        assert ok is True, (rank, ok)
+        assert n > 0
+    assert got[1][3] > 0          # rank 1 decoded a prologue
