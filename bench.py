@@ -5,17 +5,21 @@ Workload (BASELINE.json configs[2]): a synthetic 1 GiB English-text .huff --
 kjv.txt tiled (about 349.4 copies) and encoded with the files/kjv.txt.huff
 codebook, cut at a symbol boundary -- decoded on each MI355X.  One "step" is
 one full decode of that stream with the input already resident in HBM:
-hh_decode_device (k_sync + k_scan + k_emit) plus its 16-byte status
-readback.  For N > 1 the stream is N GiB, sharded by byte ranges (weak
-scaling); the shards exchange transfer tables (a tiny all-gather) before
-decoding, and the decoded segments are all-gathered once after the timed
-region (reported separately).
+hh_decode_device (one k_decode launch: speculative region decode, walks,
+transfer tables, look-back, emission) plus its status readback.  For N > 1
+the stream is N GiB, sharded by whole tiles (weak scaling); each step is
+the rank's segment decode (with its prologue tiles) plus the entry-state
+exchange (one 5-integer all-gather); the decoded segments are all-gathered
+once after the timed region and reported separately (`allgather`).
 
-Prints ONE JSON line on rank 0.  `roofline` is computed from the device-event
-duration of the decode (C + D algorithmic bytes per decode); `cpu_baseline`
-times the reference's own linApproach (oracle/_ref, compiled from the
-reference's C sources) or, if that was not built, the oracle's restatement,
-on a bounded sample (kjv.txt.huff) on one host core.
+Prints ONE JSON line on rank 0.  `roofline.achieved` = (C + D algorithmic
+bytes per decode) / the k_decode launch's average device time, measured with
+HIP events on the launch's stream inside the timed region; `traffic` is the
+HBM bytes per decode measured by rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+(profiles/pmc_latest.json, tools/gpu_profile.sh).  `cpu_baseline` times the
+reference's own linApproach (oracle/_ref, compiled from the reference's C
+sources) or, if that was not built, the oracle's restatement, on a bounded
+sample (kjv.txt.huff) on one host core.
 """
 from __future__ import annotations
 
@@ -172,8 +176,6 @@ def main():
 
     ms_step = elapsed / a.steps * 1e3
     ms_dev = statistics.mean(s["ms_total"] for s in dev_ms)
-    kern = {k: round(statistics.mean(s[k] for s in dev_ms), 4)
-            for k in ("ms_sync", "ms_scan", "ms_emit")}
     extra = {}
     if world > 1:
         extra = job.gather_report()
@@ -202,11 +204,10 @@ def main():
         "config": {"workload": workload + (f", sharded over {world} GPUs" if world > 1 else ", 1 MI355X"),
                    "compressed_bytes": C_all, "decoded_bytes": D_all,
                    "bits_per_gpu": int(C_bytes * 8), "parallelism": f"byte-range shards x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "decode pipeline k_sync+k_scan+k_emit",
+        "roofline": {"bound": "hbm", "kernel": "k_decode",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "bytes_alg": C_bytes + D_bytes, "ms_device": round(ms_dev, 4),
-                     "ms_kernels": kern},
+                     "bytes_alg": C_bytes + D_bytes, "ms_kernel": round(ms_dev, 4)},
         "decoded_MBps_device": round(D_bytes / (ms_dev * 1e-3) / 1e6, 1),
     }
     res.update(extra)
