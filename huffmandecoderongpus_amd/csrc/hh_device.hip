@@ -61,6 +61,7 @@ struct LookBack {
     uint64_t *agg;       // [ntiles] aggregate granules (table row d = 0 + CONST)
     uint64_t *inc;       // [ntiles] inclusive granules (prefix + resolved state)
     uint64_t *tabs;      // [ntiles][HH_KM] table rows d >= 1 as granules
+    uint32_t *agg32;     // [ntiles] compact aggregates (lookback_own)
     uint64_t *tdbg;      // diagnostic (HH_DEBUG_TILES): [ntiles][8] base, size|state, excl, table entry,
                          //   look-back: inclusive tile, its prefix, counts summed, rounds
 };
@@ -246,6 +247,90 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t in_st
     }
 }
 
+// Look-back that ends at this workgroup's previous tile pt (< t), whose
+// inclusive value and leaving state it computed itself: the tiles between
+// (the ones the other workgroups claimed meanwhile, about G - 1 of them)
+// need only their aggregates, all loaded in one round -- no inclusive
+// granules, no second window.  Returns false (the caller takes the general
+// look-back) when the gap is wider than 64 * HH_LBO or a tile's entering
+// state cannot be read from a CONST aggregate.
+#define HH_LBO 12
+#ifndef HH_USE_OWN
+#define HH_USE_OWN 0   // measured: ties the general look-back (register pressure); kept for study
+#endif
+// compact aggregate (u32): bit 31 published, bit 30 CONST, bits 26..29 the
+// leaving state's region d, bits 0..19 the charged count of row d = 0
+__device__ __forceinline__ uint32_t agg32_pack(uint64_t row0, bool cst) {
+    return 0x80000000u | (cst ? 0x40000000u : 0u) | (hh_state_d(hh_tab_state(row0)) << 26) |
+           ((uint32_t)hh_tab_count(row0) & 0xfffffu);
+}
+__device__ __forceinline__ int32_t agg32_count(uint32_t a) { return (int32_t)(a << 12) >> 12; }
+
+__device__ bool lookback_own(const LookBack &lb, uint64_t t, uint64_t pt, uint64_t p_incl,
+                             uint32_t p_state, uint32_t *flags, uint64_t *excl, uint32_t *st_in) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t W = t - pt - 1;                  // tiles strictly between
+    if (W > 64u * HH_LBO) return false;
+    uint32_t av[HH_LBO];
+    uint64_t a0 = 0;                                // full aggregate of tile t-1
+    uint32_t spins = 0;
+    for (;;) {
+        if (W) a0 = ld_sc1(&lb.agg[t - 1]);
+#pragma unroll
+        for (uint32_t i = 0; i < HH_LBO; i++) {
+            const uint64_t o = (uint64_t)lane * HH_LBO + i;     // tile t-1-o
+            av[i] = o < W ? __hip_atomic_load(&lb.agg32[t - 1 - o], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                          : 0x80000000u;
+        }
+        bool ready = W == 0 || (a0 >> HH_ST_SHIFT) != 0;
+#pragma unroll
+        for (uint32_t i = 0; i < HH_LBO; i++) ready = ready && (av[i] >> 31) != 0;
+        if (!__ballot(!ready)) break;
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > HH_SPIN_LIMIT) {
+            if (lane == 0) atomicOr(flags, (uint32_t)F_TIMEOUT);
+            *excl = 0;
+            *st_in = 0;
+            return true;
+        }
+    }
+    const uint32_t nxt = (uint32_t)__shfl((int)av[0], (int)((lane + 1) & 63u));   // tile below lane's last
+    bool ok = true;
+    int32_t csum = 0;
+    uint64_t rows = 0;                              // 4 bits per tile: the row d != 0 to fetch
+#pragma unroll
+    for (uint32_t i = 0; i < HH_LBO; i++) {
+        const uint64_t o = (uint64_t)lane * HH_LBO + i;
+        if (o < W) {
+            const bool oldest = o + 1 == W;                     // entered from tile pt
+            const uint32_t pv = i + 1 < HH_LBO ? av[i + 1 < HH_LBO ? i + 1 : 0] : nxt;
+            const bool known = oldest || (pv & 0x40000000u);
+            const uint32_t d = oldest ? hh_state_d(p_state) : (pv >> 26) & 0xfu;
+            ok = ok && known;
+            if (d == 0) csum += agg32_count(av[i]);
+            else rows |= (uint64_t)d << (4 * i);
+        }
+    }
+    if (__ballot(!ok)) return false;
+    while (rows) {                                  // tiles entered with d > 0: rare
+        const uint32_t i = (uint32_t)__builtin_ctzll(rows) / 4;
+        const uint32_t d = (uint32_t)(rows >> (4 * i)) & 0xfu;
+        rows &= ~(0xfull << (4 * i));
+        const uint64_t o = (uint64_t)lane * HH_LBO + i;
+        csum += hh_tab_count(poll_granule(&lb.tabs[(t - 1 - o) * HH_KM + d], flags));
+    }
+    if (W == 0) {
+        *st_in = p_state;
+    } else if (a0 & HH_CST) {
+        *st_in = hh_tab_state(a0);
+    } else {
+        return false;
+    }
+    *excl = p_incl + wave_sum64((uint64_t)(int64_t)csum);
+    return true;
+}
+
 // Stream word gi, zero past the readable payload.
 __device__ __forceinline__ uint32_t ld_word(const uint32_t *g, uint64_t gi, uint64_t nok) {
     return gi < nok ? __builtin_nontemporal_load(&g[gi]) : 0u;
@@ -359,6 +444,8 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     __shared__ int32_t s_tmp[HH_NL / 64];
     __shared__ uint32_t s_cnt[HH_NL / 64];
     __shared__ uint64_t s_bc[4];
+    __shared__ uint64_t s_own[3];              // this workgroup's last completed tile: index,
+                                               //   inclusive value, leaving state
     __shared__ uint32_t s_x[HH_NR];            // pass-1 exits and counts of the front tile
     __shared__ uint16_t s_n[HH_NR];
 
@@ -381,6 +468,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
         s_l1s[i] = (uint32_t)e;
     }
     for (uint32_t i = j; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
+    if (j == 0) s_own[0] = ~0ull;
 
     hh_ctx c;
     c.sw = SW;
@@ -402,6 +490,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     uint64_t tq = blockIdx.x + G;               // tile prefetched during that front half
     if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
 
+    uint32_t cst_seen = 0;                      // lane 0: bit 0 prologue, bit 1 emitted tiles
     LaneRec rp = {0u, 1u, 0u, 0u, 0};           // the pending tile (front done)
     uint64_t tp = ~0ull;
     uint32_t par = 0;                           // buffer parity of the next front half
@@ -420,7 +509,6 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             const uint32_t bt = c.bt;
             store_tile<SW>(pf, s_w);
             if (tq < geo.ntiles) prefetch_tile<SW>(pf, gdata, tq * tile_bits / 32, geo.nwords, geo.vec4);
-            if (j == 0 && tq < geo.ntiles) s_bc[2] = 2 * G + atomicAdd((unsigned long long *)(flags + 10), 1ull);
             __syncthreads();
             STAMP(0);
 
@@ -456,6 +544,9 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             __syncthreads();
             STAMP(7);
 #endif
+            // claim the tile after tq now; the claim's latency hides behind the table
+            uint64_t claim = 0;
+            if (j == 0 && tq < geo.ntiles) claim = atomicAdd((unsigned long long *)(flags + 10), 1ull);
             const uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt);   // barriers inside
             if (j == 0) {
                 for (uint32_t i = 0; i < nexc; i++) {
@@ -503,7 +594,10 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 for (uint32_t d = 1; d < HH_KM; d++)
                     cst = cst && hh_tab_state(s_tab[par][d]) == hh_tab_state(s_tab[par][0]);
                 st_sc1(&lb.agg[tn], HH_AGG | (cst ? HH_CST : 0ull) | s_tab[par][0]);
-                if (cst && flags[tn < geo.emit_from ? 12 : 13] == 0u) flags[tn < geo.emit_from ? 12 : 13] = 1u;
+                __hip_atomic_store(&lb.agg32[tn], agg32_pack(s_tab[par][0], cst), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                cst_seen |= cst ? (tn < geo.emit_from ? 1u : 2u) : 0u;
+                if (tq < geo.ntiles) s_bc[2] = 2 * G + claim;
             }
             rn.n = n; rn.k = kk; rn.e = wk.e; rn.cov = wk.cov; rn.delta = wk.delta;
             STAMP(3);
@@ -522,17 +616,26 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
 #ifdef HH_STAMPS
                 const uint64_t q0 = __builtin_amdgcn_s_memtime();
 #endif
-                const uint32_t sti = entering_state(lb, tp, geo.in_state, flags);
-                const uint64_t excl = tp > 0 ? lookback_excl(lb, tp, geo.in_state, geo.emit_from, flags)
-                                             : (geo.emit_from ? 0ull : (uint64_t)(int64_t)hh_state_delta(geo.in_state));
+                uint32_t sti = 0;
+                uint64_t excl = 0;
+                const uint64_t own_t = s_own[0];
+                if (!(HH_USE_OWN && own_t != ~0ull &&
+                      lookback_own(lb, tp, own_t, s_own[1], (uint32_t)s_own[2], flags, &excl, &sti))) {
+                    sti = entering_state(lb, tp, geo.in_state, flags);
+                    excl = tp > 0 ? lookback_excl(lb, tp, geo.in_state, geo.emit_from, flags)
+                                  : (geo.emit_from ? 0ull : (uint64_t)(int64_t)hh_state_delta(geo.in_state));
+                }
 #ifdef HH_STAMPS
                 COUNT(9, __builtin_amdgcn_s_memtime() - q0);
                 COUNT(10, 1);
 #endif
                 const uint64_t tab_w = s_tab[pb][hh_state_d(sti)];
+                const uint64_t incl = excl + (uint64_t)(int64_t)hh_tab_count(tab_w);
                 if (j == 0) {
-                    st_sc1(&lb.inc[tp], hh_inc_pack(excl + (uint64_t)(int64_t)hh_tab_count(tab_w),
-                                                    hh_tab_state(tab_w)));
+                    st_sc1(&lb.inc[tp], hh_inc_pack(incl, hh_tab_state(tab_w)));
+                    s_own[0] = tp;
+                    s_own[1] = incl;
+                    s_own[2] = hh_tab_state(tab_w);
                     s_bc[0] = sti;
                     s_bc[1] = excl - (uint64_t)(int64_t)hh_state_delta(sti);   // output base
                     if (tp == geo.ntiles - 1) flags[14] = hh_tab_state(tab_w);
@@ -595,6 +698,27 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 }
                 uint64_t acc = 0;
                 uint32_t nacc = 0;
+                // whole lookups while the longest possible one still ends by pe
+                const uint32_t pf = pe > geo.maxadv ? pe - geo.maxadv : 0u;
+                while (cu.p < pf) {
+                    const uint32_t win = hh_cur_win(cu);
+                    const uint32_t ix = win & (HH_L1_SIZE - 1u);
+                    const uint32_t m = c.l1m[ix];
+                    uint32_t sy = c.l1s[ix], ns = HH_M_NSYM(m), nb = HH_M_NBITS(m);
+                    if (ns == 0) {
+                        nb = hh_escape(&c, cu.p, win, &sy);
+                        ns = 1;
+                    }
+                    acc |= (uint64_t)sy << (8 * nacc);
+                    nacc += ns;
+                    if (nacc >= 4) {
+                        __builtin_nontemporal_store((uint32_t)acc, (uint32_t *)(ob + o));
+                        acc >>= 32;
+                        nacc -= 4;
+                        o += 4;
+                    }
+                    hh_cur_adv(&c, cu, nb);
+                }
                 while (cu.p < pe) {
                     hh_emit_step(&c, cu, pe, o + nacc, oend, &val, &k);
                     acc |= (uint64_t)val << (8 * nacc);
@@ -619,6 +743,11 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             tq = tq < geo.ntiles ? s_bc[2] : tq;
         }
         par ^= 1u;
+    }
+    // CONST tables seen (prologue / emitted): one store per workgroup
+    if (j == 0) {
+        if (cst_seen & 1u) flags[12] = 1u;
+        if (cst_seen & 2u) flags[13] = 1u;
     }
     STAMP_FLUSH(dbg);
 }
@@ -912,7 +1041,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     geo.vec4 = (((uintptr_t)d_data & 15u) == 0) && (geo.sw % 4 == 0);
     // workspace: [flags 64 B | agg[ntiles] | inc[ntiles] | tabs[ntiles][KM]] (zeroed)
     //            | (HH_DEBUG_TILES) tdbg[ntiles][8]
-    const size_t zero_bytes = 64 + (size_t)geo.ntiles * (16 + 8 * HH_KM);
+    const size_t zero_bytes = 64 + (size_t)geo.ntiles * (16 + 8 * HH_KM + 4);
     const int dbg_tiles = getenv("HH_DEBUG_TILES") != nullptr;
     int rc = ensure_ws(d, zero_bytes + (size_t)geo.ntiles * (dbg_tiles ? 8 : 0) * 8 + 256);
     if (rc) return rc;
@@ -922,7 +1051,8 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     lb.agg = (uint64_t *)(w + 64);
     lb.inc = lb.agg + geo.ntiles;
     lb.tabs = lb.inc + geo.ntiles;
-    lb.tdbg = dbg_tiles ? lb.tabs + geo.ntiles * HH_KM : nullptr;
+    lb.agg32 = (uint32_t *)(lb.tabs + geo.ntiles * HH_KM);
+    lb.tdbg = dbg_tiles ? (uint64_t *)(w + ((zero_bytes + 7) & ~(size_t)7)) : nullptr;
     d->last_ntiles = geo.ntiles;
     const size_t lds = lds_bytes(d);
     const kdec_t kf = kdec_for(geo.sw);
@@ -1196,7 +1326,9 @@ extern "C" int hh_debug_tiles(hh_decoder *d, uint64_t *out, int max_tiles) {
     if (!d || !out || !d->ws || !getenv("HH_DEBUG_TILES")) return 0;
     const uint64_t nt = d->last_ntiles;
     const int n = (int)(nt < (uint64_t)max_tiles ? nt : (uint64_t)max_tiles);
-    const uint64_t *src = (const uint64_t *)((uint8_t *)d->ws + 64) + nt * (2 + HH_KM);
+    // after [flags 64 B | agg | inc | tabs | agg32], 8-B aligned (decode_fast)
+    const size_t zb = 64 + (size_t)nt * (16 + 8 * HH_KM + 4);
+    const uint64_t *src = (const uint64_t *)((uint8_t *)d->ws + ((zb + 7) & ~(size_t)7));
     if (hipMemcpy(out, src, (size_t)n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         return HH_ERR_DEVICE;
     return n;
