@@ -712,7 +712,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                     acc |= (uint64_t)sy << (8 * nacc);
                     nacc += ns;
                     if (nacc >= 4) {
-                        __builtin_nontemporal_store((uint32_t)acc, (uint32_t *)(ob + o));
+                        *(uint32_t *)(ob + o) = (uint32_t)acc;
                         acc >>= 32;
                         nacc -= 4;
                         o += 4;
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                     acc |= (uint64_t)val << (8 * nacc);
                     nacc += k;
                     if (nacc >= 4) {
-                        __builtin_nontemporal_store((uint32_t)acc, (uint32_t *)(ob + o));
+                        *(uint32_t *)(ob + o) = (uint32_t)acc;
                         acc >>= 32;
                         nacc -= 4;
                         o += 4;
