@@ -978,8 +978,10 @@ static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8
                           uint64_t cap, uint64_t *out_len, hipStream_t st);
 
 static size_t lds_bytes(const hh_decoder *d) {
+    // HH_LDS_PAD_KIB: experiment knob (fewer workgroups per CU)
+    static const size_t pad = getenv("HH_LDS_PAD_KIB") ? (size_t)atoi(getenv("HH_LDS_PAD_KIB")) << 10 : 0;
     return (size_t)HH_L1_SIZE * 8 + 3 * (size_t)(d->S / 32) * HH_NLS * 4 +
-           (size_t)d->tab.l2_used * 4;
+           (size_t)d->tab.l2_used * 4 + pad;
 }
 
 // k_decode instantiated per words-per-region (S = 32 * SW bits)
