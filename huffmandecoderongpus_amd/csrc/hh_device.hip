@@ -1,23 +1,22 @@
 // hh_device.hip -- HIP kernels (gfx950) and the device half of the C ABI.
 //
 // Fast path: ONE persistent launch, k_decode (O(N) memory, 64-bit offsets).
-// Workgroup b takes tiles b, b + G, b + 2G, ... (G = resident grid).  Per
-// tile of HH_NR regions x S bits:
-//   stage     the tile's words (+ next tile's first region + a halo), loaded
-//             by each lane for its own region column one tile ahead, stored
-//             to LDS transposed (conflict-free per-lane reads)
-//   pass 1    every lane decodes its region from offset 0: count, exit
-//             (decodeallbits)
-//   walks     each exit is walked against the next region's chain until the
-//             two share a boundary: delta (makebigtable)
-//   publish   the tile's charged count sum(n + delta) -- independent of the
-//             tile's entry -- with its last exit/delta (aggregate granule)
-//   pass 2    lanes re-decode their exact runs into an LDS output window,
-//             dword writes (calcresult); windows larger than the buffer go
-//             in rounds
-//   look-back decoupled look-back over the aggregates -> output base
+// Workgroups claim tiles in order from a counter.  Per tile of HH_NR regions
+// x S bits, pipelined over two tiles (front half of tile n, back half of the
+// tile fronted one iteration earlier):
+//   stage     the tile's words (+ the next tile's first HH_KM regions and a
+//             halo), prefetched into registers one tile ahead, stored to LDS
+//             transposed (conflict-free per-lane reads)
+//   pass 1    every lane decodes its region from offset 0: count, exit and
+//             boundary mask (decodeallbits)
+//   walks     each exit is walked against the next regions' chains until
+//             they share a boundary: delta (makebigtable)
+//   publish   the tile's transfer table (charged count and leaving state for
+//             every entering state) as look-back granules
+//   look-back decoupled look-back -> entering state and output base
 //             (calcbitsindex / findmax), inclusive granule published
-//   copy      LDS window -> HBM with 16-byte aligned coalesced stores
+//   pass 2    lanes re-decode their exact runs straight to HBM, dword stores
+//             (calcresult)
 // C is read from HBM once and D written once.
 // Reference-shaped stage kernels (k_st_*) mirror the six .cl kernels one by
 // one for intermediate-array parity.
@@ -55,7 +54,16 @@ struct DevTab {
 
 // flags[0]: status bits; flags[2..3]: total symbols (u64, last tile)
 enum { F_FAIL = 1, F_OVER = 2, F_TIMEOUT = 8 };
-#define HH_SPIN_LIMIT (1u << 22)
+// A spin gives up after HH_SPIN_TICKS of the 100 MHz constant clock (4 s):
+// wall time, not iterations, so that waves descheduled by another process
+// sharing the GPU do not make a correct decode report a timeout.
+#define HH_SPIN_TICKS 400000000ull
+__device__ __forceinline__ bool spin_expired(uint32_t &spins, uint64_t &t0) {
+    if ((++spins & 255u) != 0) return false;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (t0 == 0) { t0 = now; return false; }
+    return now - t0 > HH_SPIN_TICKS;
+}
 
 struct LookBack {
     uint64_t *agg;       // [ntiles] aggregate granules (table row d = 0 + CONST)
@@ -128,13 +136,15 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
 }
 
 // Poll a granule until its status bits are non-zero (bounded).
-__device__ __forceinline__ uint64_t poll_granule(const uint64_t *p, uint32_t *flags) {
-    uint64_t v;
+// A timeout sets F_TIMEOUT and *to; the caller then emits nothing.
+__device__ __forceinline__ uint64_t poll_granule(const uint64_t *p, uint32_t *flags, bool *to) {
+    uint64_t v, t0 = 0;
     uint32_t spins = 0;
     while (((v = ld_sc1(p)) >> HH_ST_SHIFT) == 0) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > HH_SPIN_LIMIT) {
+        if (spin_expired(spins, t0)) {
             atomicOr(flags, (uint32_t)F_TIMEOUT);
+            *to = true;
             return HH_AGG;   // zero count: the decode is reported as failed
         }
     }
@@ -150,11 +160,12 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // aggregate when that is CONST (the common case: available as soon as t-1's
 // walks are done), else from its inclusive granule (t-1 resolved its own
 // entering state first).
-__device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t in_state, uint32_t *flags) {
+__device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t in_state, uint32_t *flags,
+                                   bool *to) {
     if (t == 0) return in_state;
-    const uint64_t g = poll_granule(&lb.agg[t - 1], flags);
+    const uint64_t g = poll_granule(&lb.agg[t - 1], flags, to);
     if (g & HH_CST) return hh_tab_state(g);
-    return hh_inc_state(poll_granule(&lb.inc[t - 1], flags));
+    return hh_inc_state(poll_granule(&lb.inc[t - 1], flags, to));
 }
 
 // Exclusive charged prefix of tile t (t >= 1), one wave, 64 x HH_LBV
@@ -166,7 +177,7 @@ __device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t in_s
 // of their own.
 #define HH_LBV 8   // tiles per lane per look-back round (512-tile window)
 __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t in_state, uint64_t emit_from,
-                                  uint32_t *flags) {
+                                  uint32_t *flags, bool *to) {
     constexpr uint32_t V = HH_LBV;
     const uint32_t lane = threadIdx.x & 63u;
     // tile -1: a CONST aggregate leaving in_state; its inclusive value is
@@ -182,7 +193,7 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t in_st
         const int64_t ub = top - (int64_t)(lane * V);
         uint64_t iv[V], av[V + 1];
         uint32_t ofirst, spins = 0, lf;
-        uint64_t incv;
+        uint64_t incv, t0 = 0;
         int64_t csum = 0;
         for (;;) {
 #pragma unroll
@@ -226,8 +237,9 @@ __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t in_st
             }
             if (!__ballot(!ok)) break;
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > HH_SPIN_LIMIT) {
+            if (spin_expired(spins, t0)) {
                 if (lane == 0) atomicOr(flags, (uint32_t)F_TIMEOUT);
+                *to = true;
                 return 0;
             }
         }
@@ -267,12 +279,13 @@ __device__ __forceinline__ uint32_t agg32_pack(uint64_t row0, bool cst) {
 __device__ __forceinline__ int32_t agg32_count(uint32_t a) { return (int32_t)(a << 12) >> 12; }
 
 __device__ bool lookback_own(const LookBack &lb, uint64_t t, uint64_t pt, uint64_t p_incl,
-                             uint32_t p_state, uint32_t *flags, uint64_t *excl, uint32_t *st_in) {
+                             uint32_t p_state, uint32_t *flags, uint64_t *excl, uint32_t *st_in,
+                             bool *to) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint64_t W = t - pt - 1;                  // tiles strictly between
     if (W > 64u * HH_LBO) return false;
     uint32_t av[HH_LBO];
-    uint64_t a0 = 0;                                // full aggregate of tile t-1
+    uint64_t a0 = 0, t0 = 0;                        // a0: full aggregate of tile t-1
     uint32_t spins = 0;
     for (;;) {
         if (W) a0 = ld_sc1(&lb.agg[t - 1]);
@@ -288,8 +301,9 @@ __device__ bool lookback_own(const LookBack &lb, uint64_t t, uint64_t pt, uint64
         for (uint32_t i = 0; i < HH_LBO; i++) ready = ready && (av[i] >> 31) != 0;
         if (!__ballot(!ready)) break;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > HH_SPIN_LIMIT) {
+        if (spin_expired(spins, t0)) {
             if (lane == 0) atomicOr(flags, (uint32_t)F_TIMEOUT);
+            *to = true;
             *excl = 0;
             *st_in = 0;
             return true;
@@ -318,7 +332,7 @@ __device__ bool lookback_own(const LookBack &lb, uint64_t t, uint64_t pt, uint64
         const uint32_t d = (uint32_t)(rows >> (4 * i)) & 0xfu;
         rows &= ~(0xfull << (4 * i));
         const uint64_t o = (uint64_t)lane * HH_LBO + i;
-        csum += hh_tab_count(poll_granule(&lb.tabs[(t - 1 - o) * HH_KM + d], flags));
+        csum += hh_tab_count(poll_granule(&lb.tabs[(t - 1 - o) * HH_KM + d], flags, to));
     }
     if (W == 0) {
         *st_in = p_state;
@@ -459,7 +473,6 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     const uint32_t j = threadIdx.x;
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
     const uint32_t span = HH_NCOL * S;          // bits staged per tile
-    const uint64_t G = gridDim.x;
     STAMP_DECL
 
     for (uint32_t i = j; i < HH_L1_SIZE; i += HH_NL) {
@@ -480,14 +493,17 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     c.tsym = tab.tsym;
     c.maxadv = geo.maxadv;
 
-    // Tiles are claimed in order from a counter one iteration before their
-    // front half (the first two per workgroup are blockIdx.x and +G), so the
-    // predecessors of a tile entering its back half were claimed earlier and
-    // normally have their aggregates published: no convoy behind a slow
-    // workgroup as with a fixed stride.
+    // Every tile is claimed in order from a counter, one iteration before its
+    // front half (the first two per workgroup together), so the predecessors
+    // of a tile entering its back half were claimed earlier by running
+    // workgroups and normally have their aggregates published: no convoy
+    // behind a slow workgroup as with a fixed stride, and no dependence on
+    // which workgroups are resident (a GPU shared with another process).
+    if (j == 0) s_bc[2] = atomicAdd((unsigned long long *)(flags + 10), 2ull);
+    __syncthreads();
     Prefetch pf;
-    uint64_t tn = blockIdx.x;                   // tile for the next front half
-    uint64_t tq = blockIdx.x + G;               // tile prefetched during that front half
+    uint64_t tn = s_bc[2];                      // tile for the next front half
+    uint64_t tq = tn + 1;                       // tile prefetched during that front half
     if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
 
     uint32_t cst_seen = 0;                      // lane 0: bit 0 prologue, bit 1 emitted tiles
@@ -597,7 +613,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 __hip_atomic_store(&lb.agg32[tn], agg32_pack(s_tab[par][0], cst), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
                 cst_seen |= cst ? (tn < geo.emit_from ? 1u : 2u) : 0u;
-                if (tq < geo.ntiles) s_bc[2] = 2 * G + claim;
+                if (tq < geo.ntiles) s_bc[2] = claim;
             }
             rn.n = n; rn.k = kk; rn.e = wk.e; rn.cov = wk.cov; rn.delta = wk.delta;
             STAMP(3);
@@ -618,11 +634,12 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
 #endif
                 uint32_t sti = 0;
                 uint64_t excl = 0;
+                bool to = false;                // a spin timed out: emit nothing
                 const uint64_t own_t = s_own[0];
                 if (!(HH_USE_OWN && own_t != ~0ull &&
-                      lookback_own(lb, tp, own_t, s_own[1], (uint32_t)s_own[2], flags, &excl, &sti))) {
-                    sti = entering_state(lb, tp, geo.in_state, flags);
-                    excl = tp > 0 ? lookback_excl(lb, tp, geo.in_state, geo.emit_from, flags)
+                      lookback_own(lb, tp, own_t, s_own[1], (uint32_t)s_own[2], flags, &excl, &sti, &to))) {
+                    sti = entering_state(lb, tp, geo.in_state, flags, &to);
+                    excl = tp > 0 ? lookback_excl(lb, tp, geo.in_state, geo.emit_from, flags, &to)
                                   : (geo.emit_from ? 0ull : (uint64_t)(int64_t)hh_state_delta(geo.in_state));
                 }
 #ifdef HH_STAMPS
@@ -631,6 +648,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
 #endif
                 const uint64_t tab_w = s_tab[pb][hh_state_d(sti)];
                 const uint64_t incl = excl + (uint64_t)(int64_t)hh_tab_count(tab_w);
+                const bool any_to = __ballot(to) != 0;
                 if (j == 0) {
                     st_sc1(&lb.inc[tp], hh_inc_pack(incl, hh_tab_state(tab_w)));
                     s_own[0] = tp;
@@ -638,6 +656,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                     s_own[2] = hh_tab_state(tab_w);
                     s_bc[0] = sti;
                     s_bc[1] = excl - (uint64_t)(int64_t)hh_state_delta(sti);   // output base
+                    s_bc[3] = any_to ? 1u : 0u;
                     if (tp == geo.ntiles - 1) flags[14] = hh_tab_state(tab_w);
                     if (tp == geo.emit_from) flags[15] = sti;
                     if (lb.tdbg) {
@@ -651,7 +670,6 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             const uint32_t st_in = (uint32_t)s_bc[0];
             const uint32_t d_t = hh_state_d(st_in);
             const int32_t dprev = hh_state_delta(st_in);
-            const uint64_t tab_t = s_tab[pb][d_t];
             const bool live = (mem >> d_t) & 1u;
             if (live && j + rp.k < HH_NR) {
                 s_ein[j + rp.k] = (j + rp.k) * S + rp.e;
@@ -666,13 +684,16 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             const uint32_t L = (uint32_t)block_excl_scan((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
             const uint32_t Tout = (uint32_t)Tout_i;
             const uint64_t P0 = s_bc[1];
+            // the tile's output fits [0, cap) (no wrap-around), and every
+            // granule it was based on arrived
+            const bool fits = P0 <= cap && Tout <= cap - P0 && s_bc[3] == 0;
             if (j == 0) {
                 if (tp == geo.ntiles - 1) {
                     const uint64_t tot = P0 + Tout;
                     flags[2] = (uint32_t)tot;
                     flags[3] = (uint32_t)(tot >> 32);
                 }
-                if (tp >= geo.emit_from && P0 + Tout > cap) atomicOr(flags, (uint32_t)F_OVER);
+                if (tp >= geo.emit_from && !fits) atomicOr(flags, (uint32_t)F_OVER);
                 if (lb.tdbg) {
                     lb.tdbg[tp * 8 + 0] = P0;
                     lb.tdbg[tp * 8 + 1] = Tout | ((uint64_t)st_in << 32);
@@ -685,7 +706,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             // dwords, then the ragged end
             hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
             const uint32_t y = (j + rp.k) * S + rp.e;
-            const uint32_t pe = (live && tp >= geo.emit_from && P0 + Tout <= cap) ? (y < bt ? y : bt) : 0u;
+            const uint32_t pe = (live && tp >= geo.emit_from && fits) ? (y < bt ? y : bt) : 0u;
             if (cu.p < pe) {
                 uint8_t *ob = out + P0;
                 uint32_t o = L, val, k;
