@@ -62,13 +62,13 @@
 /*   are.                                                                */
 /* ------------------------------------------------------------------ */
 #ifndef HH_NL
-#define HH_NL 256
+#define HH_NL 512
 #endif
 #define HH_NR HH_NL           /* regions per tile */
 #define HH_KM 8               /* max regions one walk may cross */
 #define HH_NCOL (HH_NR + HH_KM + 1)   /* staged columns */
 #ifndef HH_NLS
-#define HH_NLS 288            /* >= HH_NCOL, multiple of 32 */
+#define HH_NLS 544            /* >= HH_NCOL, multiple of 32 */
 #endif
 #define HH_SW_MAX 12          /* max words per region (S <= 384) */
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported

@@ -175,7 +175,9 @@ __device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t in_s
 // u-1's aggregate, which must be CONST (otherwise wait until an inclusive
 // granule appears closer); row 0 is u's aggregate, rows d > 0 are granules
 // of their own.
-#define HH_LBV 8   // tiles per lane per look-back round (512-tile window)
+#ifndef HH_LBV
+#define HH_LBV 4   // tiles per lane per look-back round (256-tile window; 8 costs 28 VGPRs)
+#endif
 __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t in_state, uint64_t emit_from,
                                   uint32_t *flags, bool *to) {
     constexpr uint32_t V = HH_LBV;
@@ -441,7 +443,17 @@ struct LaneRec {
 };
 
 template <uint32_t SW>
-__global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict__ gdata, Geometry geo,
+// Tile buffers.  2: the front half of tile n runs before the back half of
+// tile n-1 (the look-back of n-1 waits less), words, live masks and tables
+// double-buffered.  1: back half first, one buffer each -- 9 KiB less LDS per
+// workgroup, 4 workgroups per CU instead of 3.
+#ifndef HH_NBUF
+#define HH_NBUF 2
+#endif
+#ifndef HH_MINBLK
+#define HH_MINBLK 4   // waves per SIMD the register budget is sized for (<= 128 VGPRs)
+#endif
+__global__ __launch_bounds__(HH_NL, HH_MINBLK) void k_decode(const uint32_t *__restrict__ gdata, Geometry geo,
                                                      DevTab tab, LookBack lb,
                                                      uint8_t *__restrict__ out, uint64_t cap,
                                                      uint32_t *flags, uint64_t *dbg) {
@@ -449,12 +461,12 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     __shared__ uint32_t s_ein[HH_NL];          // run entries pushed by walkers
     __shared__ int16_t s_din[HH_NL];           // their deltas
     __shared__ uint16_t s_exc[HH_NL];          // exception lanes (k > 1)
-    __shared__ uint8_t s_mem[2][HH_NL];        // live masks over entering d (per pending tile)
+    __shared__ uint8_t s_mem[HH_NBUF][HH_NL];        // live masks over entering d (per pending tile)
     __shared__ uint8_t s_k[HH_NL];
     __shared__ int32_t s_part[HH_NL / 64][HH_KM];
     __shared__ int32_t s_cd[HH_KM];            // per-d counts of the partially live lanes
     __shared__ uint32_t s_ost[HH_KM];
-    __shared__ uint64_t s_tab[2][HH_KM];       // transfer table (per pending tile)
+    __shared__ uint64_t s_tab[HH_NBUF][HH_KM];       // transfer table (per pending tile)
     __shared__ int32_t s_tmp[HH_NL / 64];
     __shared__ uint32_t s_cnt[HH_NL / 64];
     __shared__ uint64_t s_bc[4];
@@ -466,8 +478,8 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     constexpr uint32_t S = 32 * SW;
     uint32_t *s_l1m = (uint32_t *)smem;                          // L1 meta halves
     uint32_t *s_l1s = s_l1m + HH_L1_SIZE;                        // L1 symbol halves
-    uint32_t *s_wb = (uint32_t *)(smem + HH_L1_SIZE * 8);       // 2 x SW * HH_NLS words
-    uint32_t *s_mk = s_wb + 2 * SW * HH_NLS;                     // SW * HH_NLS boundary-mask words
+    uint32_t *s_wb = (uint32_t *)(smem + HH_L1_SIZE * 8);       // HH_NBUF x SW * HH_NLS words
+    uint32_t *s_mk = s_wb + HH_NBUF * SW * HH_NLS;               // SW * HH_NLS boundary-mask words
     uint32_t *s_l2 = s_mk + SW * HH_NLS;
 
     const uint32_t j = threadIdx.x;
@@ -499,11 +511,14 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
     // workgroups and normally have their aggregates published: no convoy
     // behind a slow workgroup as with a fixed stride, and no dependence on
     // which workgroups are resident (a GPU shared with another process).
-    if (j == 0) s_bc[2] = atomicAdd((unsigned long long *)(flags + 10), 2ull);
+    // HH_NBUF 1 claims one tile at a time, at the end of a front half: the
+    // tile is fronted in the next iteration, right after one back half, so a
+    // back half never waits on a chain of fronts queued behind other backs.
+    if (j == 0) s_bc[2] = atomicAdd((unsigned long long *)(flags + 10), (unsigned long long)HH_NBUF);
     __syncthreads();
     Prefetch pf;
     uint64_t tn = s_bc[2];                      // tile for the next front half
-    uint64_t tq = tn + 1;                       // tile prefetched during that front half
+    uint64_t tq = tn + 1;                       // (HH_NBUF 2) tile prefetched during that front half
     if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
 
     uint32_t cst_seen = 0;                      // lane 0: bit 0 prologue, bit 1 emitted tiles
@@ -516,15 +531,17 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
         if (!front && !back) break;
         LaneRec rn = rp;
         __syncthreads();                        // buffer `par` no longer read by a back half
-        if (front) {
+        const uint32_t fb = HH_NBUF == 2 ? par : 0u, pb = HH_NBUF == 2 ? par ^ 1u : 0u;
+        auto front_half = [&]() {
             // ---------------- front half of tile tn ----------------
-            uint32_t *s_w = s_wb + par * SW * HH_NLS;
+            uint32_t *s_w = s_wb + fb * SW * HH_NLS;
             c.w = s_w;
             const uint64_t rem = geo.bits - tn * tile_bits;
             c.bt = rem < span ? (uint32_t)rem : span;
             const uint32_t bt = c.bt;
             store_tile<SW>(pf, s_w);
-            if (tq < geo.ntiles) prefetch_tile<SW>(pf, gdata, tq * tile_bits / 32, geo.nwords, geo.vec4);
+            if (HH_NBUF == 2 && tq < geo.ntiles)
+                prefetch_tile<SW>(pf, gdata, tq * tile_bits / 32, geo.nwords, geo.vec4);
             __syncthreads();
             STAMP(0);
 
@@ -550,7 +567,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
             }
             const uint32_t kk = wk.k ? wk.k : 1u;
             s_k[j] = (uint8_t)kk;
-            s_mem[par][j] = (uint8_t)hh_mem_init(j);
+            s_mem[fb][j] = (uint8_t)hh_mem_init(j);
             STAMP(2);
 
             // transfer table: live masks (exceptions, ascending, by one lane),
@@ -562,17 +579,18 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
 #endif
             // claim the tile after tq now; the claim's latency hides behind the table
             uint64_t claim = 0;
-            if (j == 0 && tq < geo.ntiles) claim = atomicAdd((unsigned long long *)(flags + 10), 1ull);
+            if (j == 0 && (HH_NBUF == 1 || tq < geo.ntiles))
+                claim = atomicAdd((unsigned long long *)(flags + 10), 1ull);
             const uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt);   // barriers inside
             if (j == 0) {
                 for (uint32_t i = 0; i < nexc; i++) {
                     const uint32_t e = s_exc[i], ke = s_k[e];
-                    const uint8_t m = s_mem[par][e];
-                    for (uint32_t q = e + 1; q < e + ke && q < HH_NR; q++) s_mem[par][q] &= (uint8_t)~m;
+                    const uint8_t m = s_mem[fb][e];
+                    for (uint32_t q = e + 1; q < e + ke && q < HH_NR; q++) s_mem[fb][q] &= (uint8_t)~m;
                 }
             }
             __syncthreads();
-            const uint32_t mem = s_mem[par][j];
+            const uint32_t mem = s_mem[fb][j];
             const int32_t charged = (int32_t)(n + wk.cov) + wk.delta;
             if (j + kk >= HH_NR) {
                 const uint32_t os = hh_state_pack(j + kk - HH_NR, wk.e, wk.delta);
@@ -599,7 +617,7 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 // entry correction of the first emitted tile instead
                 if (tn < geo.emit_from) cnt = tn + 1 == geo.emit_from ? hh_state_delta(s_ost[j]) : 0;
                 const uint64_t row = hh_tab_pack(cnt, s_ost[j]);
-                s_tab[par][j] = row;
+                s_tab[fb][j] = row;
                 if (j > 0) st_sc1(&lb.tabs[tn * HH_KM + j], HH_AGG | row);
             }
             __syncthreads();
@@ -608,20 +626,19 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 // the same for every entering d)
                 bool cst = true;
                 for (uint32_t d = 1; d < HH_KM; d++)
-                    cst = cst && hh_tab_state(s_tab[par][d]) == hh_tab_state(s_tab[par][0]);
-                st_sc1(&lb.agg[tn], HH_AGG | (cst ? HH_CST : 0ull) | s_tab[par][0]);
-                __hip_atomic_store(&lb.agg32[tn], agg32_pack(s_tab[par][0], cst), __ATOMIC_RELAXED,
+                    cst = cst && hh_tab_state(s_tab[fb][d]) == hh_tab_state(s_tab[fb][0]);
+                st_sc1(&lb.agg[tn], HH_AGG | (cst ? HH_CST : 0ull) | s_tab[fb][0]);
+                __hip_atomic_store(&lb.agg32[tn], agg32_pack(s_tab[fb][0], cst), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
                 cst_seen |= cst ? (tn < geo.emit_from ? 1u : 2u) : 0u;
-                if (tq < geo.ntiles) s_bc[2] = claim;
+                if (HH_NBUF == 1 || tq < geo.ntiles) s_bc[2] = claim;
             }
             rn.n = n; rn.k = kk; rn.e = wk.e; rn.cov = wk.cov; rn.delta = wk.delta;
             STAMP(3);
-        }
+        };
 
-        if (back) {
+        auto back_half = [&]() {
             // ---------------- back half of tile tp ----------------
-            const uint32_t pb = par ^ 1u;
             c.w = s_wb + pb * SW * HH_NLS;
             const uint64_t rem = geo.bits - tp * tile_bits;
             c.bt = rem < span ? (uint32_t)rem : span;
@@ -754,14 +771,27 @@ __global__ __launch_bounds__(HH_NL, 3) void k_decode(const uint32_t *__restrict_
                 for (uint32_t i = 0; i < nacc; i++) ob[o + i] = (uint8_t)(acc >> (8 * i));
             }
             STAMP(6);
-        }
+        };
+#if HH_NBUF == 2
+        if (front) front_half();
+        if (back) back_half();
+#else
+        if (back) back_half();
+        __syncthreads();                        // tile tp's words and tables no longer read
+        if (front) front_half();
+#endif
         // the front half's tile becomes the pending one
         rp = rn;
         tp = front ? tn : ~0ull;
         if (front) {
-            tn = tq;
             __syncthreads();                    // s_bc[2] (claimed by lane 0) visible
-            tq = tq < geo.ntiles ? s_bc[2] : tq;
+            if (HH_NBUF == 2) {
+                tn = tq;
+                tq = tq < geo.ntiles ? s_bc[2] : tq;
+            } else {
+                tn = s_bc[2];
+                if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
+            }
         }
         par ^= 1u;
     }
@@ -1001,7 +1031,7 @@ static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8
 static size_t lds_bytes(const hh_decoder *d) {
     // HH_LDS_PAD_KIB: experiment knob (fewer workgroups per CU)
     static const size_t pad = getenv("HH_LDS_PAD_KIB") ? (size_t)atoi(getenv("HH_LDS_PAD_KIB")) << 10 : 0;
-    return (size_t)HH_L1_SIZE * 8 + 3 * (size_t)(d->S / 32) * HH_NLS * 4 +
+    return (size_t)HH_L1_SIZE * 8 + (HH_NBUF + 1) * (size_t)(d->S / 32) * HH_NLS * 4 +
            (size_t)d->tab.l2_used * 4 + pad;
 }
 

@@ -25,6 +25,9 @@
 
 extern "C" {
 
+// regions per tile of the emulated (and the kernel's) geometry
+uint32_t hh_emu_regions(void) { return HH_NR; }
+
 
 // stats[0]=tiles stats[1]=walks with k > 1 stats[2]=failed walks
 // stats[3]=region bits used stats[4]=max k stats[5]=non-CONST tiles

@@ -23,6 +23,7 @@ def _emu():
                                       C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32,
                                       C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
                                       C.c_void_p])
+    L.hh_emu_regions.restype = C.c_uint32
     return L
 
 
@@ -42,7 +43,7 @@ def emu_segment(L, tree, payload, seg, in_state, prologue):
     st = np.zeros(8, np.int64)
     leave, entry = C.c_uint32(0), C.c_uint32(0)
     n = L.hh_emu_decode_range(tree.izero.ctypes.data, tree.ione.ctypes.data, tree.sym.ctypes.data,
-                              len(tree.izero), d.ctypes.data, bits, seg.tile_bits // 256,
+                              len(tree.izero), d.ctypes.data, bits, seg.tile_bits // L.hh_emu_regions(),
                               seg.ntiles - skip, prologue, in_state, out.ctypes.data, len(out),
                               st.ctypes.data, C.byref(leave), C.byref(entry))
     assert n >= 0, n
@@ -63,7 +64,7 @@ def _worker(rank, world, port, probe, name, q):
         hf = H.HuffFile.load(os.path.join(FILES, name + ".huff"))
         tree = hf.tree()
         L = _emu()
-        seg = shard.plan(hf.bits, 256 * 256, world, rank, probe)
+        seg = shard.plan(hf.bits, L.hh_emu_regions() * 256, world, rank, probe)
 
         def gather(vals):
             t = torch.tensor(vals, dtype=torch.int64)
