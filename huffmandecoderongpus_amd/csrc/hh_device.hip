@@ -176,7 +176,8 @@ __device__ uint32_t entering_state(const LookBack &lb, uint64_t t, uint32_t in_s
 // granule appears closer); row 0 is u's aggregate, rows d > 0 are granules
 // of their own.
 #ifndef HH_LBV
-#define HH_LBV 4   // tiles per lane per look-back round (256-tile window; 8 costs 28 VGPRs)
+#define HH_LBV 2   // tiles per lane per look-back round (128-tile window). Same-box A/B on
+                   // the 1 GiB stream: 1 -> 5.75 ms, 2 -> 5.67 ms, 4 -> 5.83 ms; 8 costs 28 VGPRs
 #endif
 __device__ uint64_t lookback_excl(const LookBack &lb, uint64_t t, uint32_t in_state, uint64_t emit_from,
                                   uint32_t *flags, bool *to) {
