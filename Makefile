@@ -57,9 +57,3 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all lib cli emu oracle clean
-
-# diagnostic build: per-phase s_memtime stamps (tools/diag_stamps.py)
-stamps: $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
-	$(HIPCC) -DHH_STAMPS $(HIPFLAGS) -c $(CSRC)/hh_device.hip -o $(BUILD)/hh_device_stamps.o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/libhiphuff_stamps.so $(BUILD)/hh_device_stamps.o $^
-.PHONY: stamps

@@ -108,14 +108,47 @@ def load_pmc(path: str, workload: str):
     return None
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a) -> int:
+    """`bench.py --gpus N` started as a plain process (WORLD_SIZE unset):
+    start N ranks under torch.distributed.run as a CHILD process -- before
+    anything here touches the GPU -- and return its exit code.  Fails loudly
+    when the node has fewer than N GPUs (torch.cuda.device_count() does not
+    initialise the GPU on this image)."""
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()
+    if have < a.gpus:
+        raise SystemExit(f"bench.py --gpus {a.gpus}: only {have} GPU(s) visible on this node")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = _args()
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:
+        if a.gpus > 1:
+            sys.exit(launch_ranks(a))
+        world = 1
+    if world != a.gpus:
+        raise SystemExit(f"bench.py --gpus {a.gpus} but WORLD_SIZE={world}")
     import torch
     import torch.distributed as dist
     import huffmandecoderongpus_amd as H
     from huffmandecoderongpus_amd import synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -148,6 +181,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         ok = job.verify()
+        D_bytes = job.decoded_bytes       # known once the shard has been decoded
     else:
         ok = n == syn.decoded_bytes and synth.verify_tiled(out, syn)
     if not ok:
@@ -176,6 +210,9 @@ def main():
 
     ms_step = elapsed / a.steps * 1e3
     ms_dev = statistics.mean(s["ms_total"] for s in dev_ms)
+    phases = {k: round(statistics.mean(s[f"ms_{k}"] for s in dev_ms), 4)
+              for k in ("sync", "scan", "emit")}
+    fast = all(s["exact_fallback"] == 0 for s in dev_ms)
     extra = {}
     if world > 1:
         extra = job.gather_report()
@@ -204,11 +241,14 @@ def main():
         "config": {"workload": workload + (f", sharded over {world} GPUs" if world > 1 else ", 1 MI355X"),
                    "compressed_bytes": C_all, "decoded_bytes": D_all,
                    "bits_per_gpu": int(C_bytes * 8), "parallelism": f"byte-range shards x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_decode",
+        "roofline": {"bound": "hbm", "kernel": "k_front+k_scan1+k_scan2+k_emit",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "bytes_alg": C_bytes + D_bytes, "ms_kernel": round(ms_dev, 4)},
+                     "bytes_alg": C_bytes + D_bytes, "ms_kernel": round(ms_dev, 4),
+                     "ms_front": phases["sync"], "ms_scan": phases["scan"],
+                     "ms_emit": phases["emit"]},
         "decoded_MBps_device": round(D_bytes / (ms_dev * 1e-3) / 1e6, 1),
+        "fast_path": fast,
     }
     res.update(extra)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -116,7 +116,6 @@ _SIGS = {
     "hh_stage_pipeline": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint64,
                            C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
     "hipHuffApproach": ([C.c_void_p, C.c_void_p, C.c_void_p], None),
-    "hh_debug_phase_cycles": ([C.c_void_p, C.c_void_p, C.c_int], C.c_int),
 }
 
 
@@ -254,12 +253,6 @@ class Decoder:
         st = _Stats()
         _check(lib().hh_decoder_stats(self._h, C.byref(st)), "stats")
         return {k: getattr(st, k) for k, _ in _Stats._fields_}
-
-    def phase_cycles(self, max_blocks: int = 4096) -> np.ndarray:
-        """Diagnostic (HH_STAMPS builds): per-block cycles of each phase."""
-        buf = np.zeros((max_blocks, 12), np.uint64)
-        n = lib().hh_debug_phase_cycles(self._h, buf.ctypes.data, max_blocks)
-        return buf[: max(n, 0)]
 
     def decode_host(self, payload: np.ndarray, bits: int, cap: int) -> np.ndarray:
         payload = np.ascontiguousarray(payload, np.uint8)

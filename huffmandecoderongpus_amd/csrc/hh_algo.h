@@ -62,13 +62,13 @@
 /*   are.                                                                */
 /* ------------------------------------------------------------------ */
 #ifndef HH_NL
-#define HH_NL 512
+#define HH_NL 256
 #endif
 #define HH_NR HH_NL           /* regions per tile */
 #define HH_KM 8               /* max regions one walk may cross */
 #define HH_NCOL (HH_NR + HH_KM + 1)   /* staged columns */
 #ifndef HH_NLS
-#define HH_NLS 544            /* >= HH_NCOL, multiple of 32 */
+#define HH_NLS 288            /* >= HH_NCOL, multiple of 32 */
 #endif
 #define HH_SW_MAX 12          /* max words per region (S <= 384) */
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
@@ -94,6 +94,9 @@ HH_HD uint32_t hh_lowmask(uint32_t o) { return o >= 32 ? 0xffffffffu : ((1u << o
 #define HH_M_NSYM(m) (((m) >> 5) & 7u)
 #define HH_M_LEN0(m) (((m) >> 8) & 31u)
 #define HH_M_BMASK(m) (((m) >> 13) & 0x7ffu)
+/* escape meta word (nsym == 0): the L2 subtable */
+#define HH_M_L2BASE(m) (((m) >> 8) & 0xffffu)
+#define HH_M_L2Q(m) (((m) >> 24) & 31u)
 
 HH_HD uint32_t hh_magic(uint32_t sw) { return (uint32_t)((0x100000000ull + sw - 1) / sw); }
 
@@ -166,9 +169,8 @@ HH_HD uint32_t hh_tail_symbol(const hh_ctx *c, uint32_t p) {
 /* First code longer than HH_P bits: second-level table, then (very long
  * codes only) a bit-serial walk.  Returns the code length.  A walk that
  * hits the end of the stream returns the cut-off length. */
-HH_HD uint32_t hh_escape(const hh_ctx *c, uint32_t p, uint32_t win, uint32_t *sym) {
-    const uint32_t e = c->l1s[win & (HH_L1_SIZE - 1u)];
-    uint32_t q = HH_L1_L2Q(e), base = HH_L1_L2BASE(e);
+HH_HD uint32_t hh_escape(const hh_ctx *c, uint32_t p, uint32_t win, uint32_t m, uint32_t *sym) {
+    uint32_t q = HH_M_L2Q(m), base = HH_M_L2BASE(m);
     uint32_t e2 = c->l2[base + ((win >> HH_P) & ((1u << q) - 1u))];
     if (e2 & HH_L2_LEAF) {
         *sym = e2 & 0xffu;
@@ -200,10 +202,12 @@ HH_HD hh_look hh_lookup_w(const hh_ctx *c, uint32_t p, uint32_t win) {
         L.nb = HH_M_NBITS(m);
         L.bm = HH_M_BMASK(m);
         L.len0 = HH_M_LEN0(m);
-        L.syms = c->l1s[win & (HH_L1_SIZE - 1u)];
+        /* the front kernel stages only the meta half (l1s null): it never
+         * needs the symbol bytes */
+        L.syms = c->l1s ? c->l1s[win & (HH_L1_SIZE - 1u)] : 0u;
     } else {
         uint32_t s;
-        L.nb = L.len0 = hh_escape(c, p, win, &s);
+        L.nb = L.len0 = hh_escape(c, p, win, m, &s);
         L.ns = 1;
         L.bm = 1;
         L.syms = s;
@@ -275,7 +279,7 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
         uint32_t ns = HH_M_NSYM(m), nb = HH_M_NBITS(m), bm = HH_M_BMASK(m);
         if (ns == 0) {
             uint32_t s;
-            nb = hh_escape(c, u.p, win, &s);
+            nb = hh_escape(c, u.p, win, m, &s);
             ns = 1;
             bm = 1;
         }
@@ -379,7 +383,7 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
                 uint32_t lns = HH_M_NSYM(m), lnb = HH_M_NBITS(m), lbm = HH_M_BMASK(m);
                 if (lns == 0) {
                     uint32_t sy;
-                    lnb = hh_escape(c, u.p, win, &sy);
+                    lnb = hh_escape(c, u.p, win, m, &sy);
                     lns = 1;
                     lbm = 1;
                 }

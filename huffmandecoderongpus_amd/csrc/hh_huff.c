@@ -381,7 +381,11 @@ int hh_tables_build(const void *tree_v, hh_tables *T) {
                 }
             }
             T->l2_used = base + (1u << q);
-            e = (uint64_t)base | ((uint64_t)q << 16);
+            /* the subtable reference sits in both halves: the meta half's
+             * nsym field stays 0 (escape), so a pass that stages only the
+             * meta half (the front kernel) still finds its subtable */
+            e = (uint64_t)base | ((uint64_t)q << 16) |
+                ((uint64_t)(((uint32_t)base << 8) | ((uint32_t)q << 24)) << 32);
         }
         T->l1[w] = e;
     }

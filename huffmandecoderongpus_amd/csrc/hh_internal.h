@@ -16,6 +16,9 @@
  *     escape entries (nsym == 0):
  *     bits  0..15  L2 base index of the subtable for the depth-HH_P node
  *     bits 16..20  q: index bits of that subtable (<= HH_Q_MAX)
+ *     bits 40..55  the same L2 base, bits 56..60 the same q (so the meta
+ *                  half alone -- all the front kernel stages -- resolves
+ *                  an escape; bits 37..39 stay 0)
  *   A multi-symbol entry is the reference's bigTableMulti idea
  *   (mainrun.c:197-201, 229-247) restricted to the bits in the window.
  *

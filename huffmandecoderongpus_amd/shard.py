@@ -158,6 +158,11 @@ class ShardJob:
 
     def _decode(self, in_state: int, prologue: int) -> dict:
         s = self.seg
+        if s.t1 == s.t0:
+            # no owned tile (fewer tiles than ranks): nothing to decode, and
+            # the chain leaves this rank in the state it entered
+            return {"out_len": 0, "leave_state": in_state, "const_seen": False,
+                    "entry_state": in_state, "entry_exact": prologue == 0, "in_state": in_state}
         skip = (s.prologue - prologue) * s.tile_bits          # bits, multiple of 32
         r = self.dec.decode_range_ptr(self.syn.data.data_ptr() + skip // 8,
                                       s.bits_avail - skip, s.ntiles - (s.prologue - prologue),

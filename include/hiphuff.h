@@ -125,8 +125,10 @@ typedef struct {
     int flags;               /* HH_FLAG_*                                    */
 } hh_config;
 
-#define HH_FLAG_FORCE_EXACT 1   /* skip the sync fast path, use the exact
-                                   transfer-function path throughout */
+#define HH_FLAG_FORCE_EXACT 1   /* skip the fast path and decode with the
+                                   reference-shaped stage pipeline (the six
+                                   hh_stage_* kernels: exact, O(25 * bits)
+                                   memory, bits < 2^31) */
 
 int hh_decoder_create(hh_decoder **dec, const hh_config *cfg);
 void hh_decoder_destroy(hh_decoder *dec);
@@ -138,13 +140,17 @@ int hh_decoder_set_tree(hh_decoder *dec, const hh_tree *tree);
 /* Statistics of the last decode (device time of each phase, in ms). */
 typedef struct {
     double ms_total;         /* hipEvent time of the whole device pipeline  */
-    double ms_sync;          /* speculative decode + chain stitching        */
-    double ms_scan;          /* offsets                                      */
-    double ms_emit;          /* symbol emission                              */
+    double ms_sync;          /* front kernel: speculative region decode,
+                                walks, tile transfer tables                 */
+    double ms_scan;          /* scan kernels: tile entering states, offsets */
+    double ms_emit;          /* emit kernel: exact runs decoded to HBM      */
     uint64_t out_len;        /* symbols decoded                              */
     uint64_t lanes;          /* lane regions                                 */
-    uint64_t repairs;        /* lane walks that needed a repair              */
-    int exact_fallback;      /* 1 if the transfer-function path was used    */
+    uint64_t repairs;        /* 1: a tile-state chain was composed on the
+                                host (or the stage pipeline ran)            */
+    int exact_fallback;      /* 1 if the stage pipeline decoded (a code the
+                                fast path does not take, or a walk that
+                                found no merge)                             */
 } hh_stats;
 
 int hh_decoder_stats(const hh_decoder *dec, hh_stats *st);

@@ -48,6 +48,7 @@ def test_fixture_device(hh, dec, files_dir, name):
     d_out = torch.zeros(hf.uncompressedsize + 64, dtype=torch.uint8, device="cuda")
     n = dec.decode_device(d_in, hf.bits, d_out)
     torch.cuda.synchronize()
+    assert dec.stats()["exact_fallback"] == 0      # the fast path decoded it
     assert n == len(ref)
     assert np.array_equal(d_out[:n].cpu().numpy(), ref)
     assert int(d_out[n:].sum().item()) == 0   # nothing written past the end
@@ -210,7 +211,6 @@ def test_segments_concatenate(hh, files_dir, world, probe):
     "rank" is a thread running shard.settle over an in-process gather (one
     decoder, calls serialised).  probe 0: entries are guesses that the
     exchange must catch.  The outputs must concatenate to the oracle's."""
-    import threading
     import torch
     from huffmandecoderongpus_amd import shard
     path = os.path.join(files_dir, "kjv.txt.huff")
@@ -224,25 +224,50 @@ def test_segments_concatenate(hh, files_dir, world, probe):
         pay[:len(hf.payload)] = torch.from_numpy(hf.payload.copy()).cuda()
         segs = [shard.plan(hf.bits, tb, world, r, probe) for r in range(world)]
         outs = [torch.zeros(hf.bits + 64, dtype=torch.uint8, device="cuda") for _ in segs]
-        lock = threading.Lock()
-        bar = threading.Barrier(world)
-        slots = [None] * world
-        final = [None] * world
-        redone = [0] * world
+        final, redone = _settle_segments(dec, pay, segs, outs)
+        got = torch.cat([outs[r][:final[r]["out_len"]] for r in range(world)]).cpu().numpy()
+        assert len(got) == len(ref) and np.array_equal(got, ref)
+        if probe:
+            assert sum(redone) == 0
+        else:
+            assert sum(redone) >= 1
+    finally:
+        dec.close()
 
-        def run(r, in_state, prologue):
-            s = segs[r]
-            skip = s.prologue - prologue
-            with lock:
-                res = dec.decode_range_ptr(pay.data_ptr() + (s.buf_bit + skip * tb) // 8,
-                                           s.bits_avail - skip * tb, s.ntiles - skip, in_state,
-                                           outs[r].data_ptr(), outs[r].numel(), 0,
-                                           prologue=prologue)
-                torch.cuda.synchronize()
-            res["in_state"] = res["entry_state"]
-            return res
 
-        def rank_main(r):
+def _settle_segments(dec, pay, segs, outs):
+    """Every segment decoded with hh_decode_device_range on this one GPU, one
+    thread per "rank" running shard.settle over an in-process gather (calls
+    serialised on one decoder).  Returns (final results, redo counts)."""
+    import threading
+    import torch
+    from huffmandecoderongpus_amd import shard
+    world = len(segs)
+    tb = segs[0].tile_bits
+    lock = threading.Lock()
+    bar = threading.Barrier(world)
+    slots = [None] * world
+    final = [None] * world
+    redone = [0] * world
+    errors = []
+
+    def run(r, in_state, prologue):
+        s = segs[r]
+        skip = s.prologue - prologue
+        if s.t1 == s.t0:
+            return {"out_len": 0, "leave_state": in_state, "const_seen": False,
+                    "entry_state": in_state, "entry_exact": prologue == 0, "in_state": in_state}
+        with lock:
+            res = dec.decode_range_ptr(pay.data_ptr() + (s.buf_bit + skip * tb) // 8,
+                                       s.bits_avail - skip * tb, s.ntiles - skip, in_state,
+                                       outs[r].data_ptr(), outs[r].numel(), 0,
+                                       prologue=prologue)
+            torch.cuda.synchronize()
+        res["in_state"] = res["entry_state"]
+        return res
+
+    def rank_main(r):
+        try:
             def gather(vals):
                 slots[r] = list(vals)
                 bar.wait()
@@ -258,20 +283,55 @@ def test_segments_concatenate(hh, files_dir, world, probe):
             if segs[r].prologue == 0 and segs[r].t0 > 0:
                 first["entry_exact"] = False
             final[r] = shard.settle(first, redo, gather, r, world)[0]
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+            bar.abort()
 
-        th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join(timeout=120)
-        got = torch.cat([outs[r][:final[r]["out_len"]] for r in range(world)]).cpu().numpy()
-        assert len(got) == len(ref) and np.array_equal(got, ref)
-        if probe:
-            assert sum(redone) == 0
-        else:
-            assert sum(redone) >= 1
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    return final, redone
+
+
+def test_eight_shards_of_the_8gib_stream():
+    """BASELINE.json configs[3] on one GPU: the 8 GiB kjv-tiled stream cut
+    into the 8 shards bench.py --gpus 8 plans (1 GiB each, 2 prologue
+    tiles), every shard decoded with hh_decode_device_range, entry states
+    settled; each shard's output must equal the tiled text from its base and
+    the bases must add up to the whole stream's symbol count."""
+    import torch
+    from huffmandecoderongpus_amd import shard, synth
+    H = pytest.importorskip("huffmandecoderongpus_amd")
+    hf, text = synth.load_source(os.path.join(ROOT, "files"))
+    world = 8
+    syn = synth.tiled_stream(hf, text, world << 30)
+    dec = H.Decoder(0)
+    try:
+        dec.set_tree(syn.tree)
+        tb = dec.tile_bits()
+        segs = [shard.plan(syn.bits, tb, world, r) for r in range(world)]
+        minlen = int(min(v for v in synth.code_lengths(syn.tree) if v > 0))
+        outs = [torch.empty(s.owned_bits // minlen + 4096, dtype=torch.uint8, device="cuda")
+                for s in segs]
+        final, redone = _settle_segments(dec, syn.data, segs, outs)
+        assert sum(redone) == 0                       # every prologue was exact
+        L = syn.text.numel()
+        base = 0
+        for r in range(world):
+            n = final[r]["out_len"]
+            for o in range(0, n, 1 << 28):
+                m = min(1 << 28, n - o)
+                idx = (torch.arange(m, device="cuda", dtype=torch.int64) + (base + o)) % L
+                assert torch.equal(outs[r][o:o + m], syn.text[idx]), (r, o)
+            base += n
+        assert base == syn.decoded_bytes
     finally:
         dec.close()
+        del outs
+        torch.cuda.empty_cache()
 
 
 def _shard_rank(rank, world, port, mib, q):
