@@ -41,6 +41,8 @@
 #define HH_NW (HH_NL / 64)          // waves per workgroup
 #define HH_SCAN_TB 1024             // tiles per k_scan1 block
 #define HH_SCAN_BACK 4096           // longest non-CONST chain k_scan1 composes (else host scan)
+#define HH_OB (16384 + 64)          // k_emit's LDS output staging (bytes): a text tile's output
+                                    // (<= ~15.2 K symbols for kjv) plus the 16-B phase
 
 #define HIP_OK(x)                                                             \
     do {                                                                      \
@@ -460,7 +462,8 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     uint32_t *s_l1m = (uint32_t *)smem;
     uint32_t *s_l1s = s_l1m + HH_L1_SIZE;
     uint32_t *s_w = s_l1s + HH_L1_SIZE;                 // SW * HH_NLS words (transposed)
-    uint32_t *s_l2 = s_w + SW * HH_NLS;
+    uint32_t *s_out = s_w + SW * HH_NLS;                // HH_OB bytes of output staging
+    uint32_t *s_l2 = s_out + HH_OB / 4;
 
     const uint32_t j = threadIdx.x;
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
@@ -516,12 +519,79 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
         const bool fits = P0s >= 0 && P0 <= cap && Tout <= cap - P0;
         if (j == 0 && !fits) atomicOr(wk.flags, (uint32_t)F_OVER);
 
-        // this lane's symbols, straight to HBM (output bytes [P0 + L, P0 +
-        // L + rc)); bytes up to a dword boundary, then dwords, then the
-        // ragged end
         hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
         const uint32_t y = (j + kk) * S + ee;
         const uint32_t pe = (live && fits) ? (y < bt ? y : bt) : 0u;
+        // The tile's output [P0, P0 + Tout) is staged in LDS at byte a0 =
+        // P0 mod 16, so that 16-B blocks of LDS and of HBM line up: lanes
+        // OR their symbols in as dwords (a dword two runs share needs the
+        // OR; the buffer is zeroed first), then the block copies it out with
+        // whole 16-B stores -- every line written once, by one instruction.
+        const uint32_t a0 = (uint32_t)(P0 & 15u);
+#ifndef HH_NO_STAGE
+        if (fits && a0 + Tout <= HH_OB) {
+#else
+        if (false) {
+#endif
+            const uint32_t nq = (a0 + Tout + 15u) / 16u;
+            for (uint32_t i = j; i < nq; i += HH_NL) *(u32x4 *)(s_out + 4 * i) = (u32x4){0u, 0u, 0u, 0u};
+            __syncthreads();
+            if (cu.p < pe) {
+                const uint32_t b = a0 + L;
+                uint32_t wd = b >> 2, nacc = b & 3u, emitted = 0, val, k;
+                uint64_t acc = 0;
+                const uint32_t pf_end = pe > geo.maxadv ? pe - geo.maxadv : 0u;
+                while (cu.p < pf_end) {            // whole lookups
+                    const uint32_t win = hh_cur_win(cu);
+                    const uint32_t ix = win & (HH_L1_SIZE - 1u);
+                    const uint32_t m = c.l1m[ix];
+                    uint32_t sy = c.l1s[ix], ns = HH_M_NSYM(m), nb = HH_M_NBITS(m);
+                    if (ns == 0) {
+                        nb = hh_escape(&c, cu.p, win, m, &sy);
+                        ns = 1;
+                    }
+                    acc |= (uint64_t)sy << (8 * nacc);
+                    nacc += ns;
+                    emitted += ns;
+                    if (nacc >= 4) {
+                        atomicOr(&s_out[wd], (uint32_t)acc);
+                        wd++;
+                        acc >>= 32;
+                        nacc -= 4;
+                    }
+                    hh_cur_adv(&c, cu, nb);
+                }
+                while (cu.p < pe) {                // the end of the run (and of the stream)
+                    hh_emit_step(&c, cu, pe, emitted, rc, &val, &k);
+                    acc |= (uint64_t)val << (8 * nacc);
+                    nacc += k;
+                    emitted += k;
+                    if (nacc >= 4) {
+                        atomicOr(&s_out[wd], (uint32_t)acc);
+                        wd++;
+                        acc >>= 32;
+                        nacc -= 4;
+                    }
+                }
+                if (nacc) atomicOr(&s_out[wd], (uint32_t)acc);
+            }
+            __syncthreads();
+            uint8_t *gb = out + (P0 - a0);
+            const uint8_t *sb = (const uint8_t *)s_out;
+            for (uint32_t i = j; i < nq; i += HH_NL) {
+                const uint32_t lo = 16 * i;
+                if (lo >= a0 && lo + 16 <= a0 + Tout) {
+                    __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
+                } else {                           // a block shared with a neighbouring tile
+                    const uint32_t e = lo + 16 < a0 + Tout ? lo + 16 : a0 + Tout;
+                    for (uint32_t q = lo > a0 ? lo : a0; q < e; q++) gb[q] = sb[q];
+                }
+            }
+            continue;
+        }
+        // a tile too large for the staging buffer: this lane's symbols
+        // straight to HBM (output bytes [P0 + L, P0 + L + rc)); bytes up to a
+        // dword boundary, then dwords, then the ragged end
         if (cu.p < pe) {
             uint8_t *ob = out + P0;
             uint32_t o = L, val, k;
@@ -762,7 +832,17 @@ static uint32_t pick_region_bits(const hh_tables *t, int req) {
         if (req % 32 || req > 32 * HH_SW_MAX) return 0;
         return (uint32_t)req;
     }
-    return hh_pick_region_bits(g);
+    uint32_t S = hh_pick_region_bits(g);
+    // A fixed-length code puts HH_NR * S / len symbols in every tile: keep
+    // that within k_emit's staging buffer (E.coli: 2-bit codes, S = 128).
+    if (t->fixed_len > 0 && S) {
+        uint32_t x = 32, y = g;
+        while (y) { const uint32_t r = x % y; x = y; y = r; }
+        const uint32_t lcm = 32 / x * g;
+        const uint64_t smax = (uint64_t)(HH_OB - 64) * (uint32_t)t->fixed_len / HH_NR;
+        while (S > smax && S > lcm) S -= lcm;
+    }
+    return S;
 }
 
 extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
@@ -809,7 +889,7 @@ static size_t lds_front(uint32_t sw, uint32_t l2) {
     return ((size_t)HH_L1_SIZE + 2 * (size_t)sw * HH_NLS + l2) * 4;
 }
 static size_t lds_emit(uint32_t sw, uint32_t l2) {
-    return (2 * (size_t)HH_L1_SIZE + (size_t)sw * HH_NLS + l2) * 4;
+    return (2 * (size_t)HH_L1_SIZE + (size_t)sw * HH_NLS + l2) * 4 + HH_OB;
 }
 
 // kernels instantiated per words-per-region (S = 32 * SW bits)

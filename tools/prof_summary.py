@@ -1,10 +1,16 @@
-"""Summarise tools/gpu_profile.sh output (gpurun_out/prof) into profiles/.
+"""Summarise tools/profile.sh output (gpurun_out/prof/<tag>) into profiles/.
 
-Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim),
-profiles/<tag>_k_decode.json (k_decode durations, HBM bytes, SQ counters)
-and profiles/pmc_latest.json (read by bench.py for roofline.traffic).
-HBM bytes per decode = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
-FETCH_SIZE counts half the bytes of a coalesced read (MI355X_MICROARCH.md, HBM).
+    python tools/prof_summary.py <tag> [workload]
+
+Writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, verbatim) and
+profiles/<tag>_kernels.json: per kernel of the decode pipeline (k_front,
+k_scan1, k_scan2, k_emit) the mean dispatch duration, HBM bytes per dispatch
+and the SQ counters, over the bench-sized dispatches (those at least half as
+long as the longest of that kernel).  HBM bytes per dispatch = 2 x FETCH_SIZE
++ WRITE_SIZE (KiB -> bytes): on gfx950 FETCH_SIZE counts half the bytes of a
+coalesced read (MI355X_MICROARCH.md, HBM).  Also writes
+profiles/pmc_latest.json (read by bench.py for roofline.traffic: the whole
+pipeline's bytes per decode).
 """
 import csv
 import glob
@@ -15,76 +21,78 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF = os.path.join(ROOT, "gpurun_out", "prof")
-KERNEL = "k_decode"
+KERNELS = ("k_front", "k_scan1", "k_scan2", "k_emit")
 
 
-def find(sub, pat):
-    hits = glob.glob(os.path.join(PROF, sub, "**", pat), recursive=True)
-    if not hits:
-        raise SystemExit(f"no {pat} under {sub}")
-    return hits[0]
+def kname(s):
+    for k in KERNELS:
+        if k in s:
+            return k
+    return None
 
 
-def rows(path):
-    with open(path) as f:
-        return list(csv.DictReader(f))
-
-
-def big(vals):
-    """The bench-sized dispatches: the run also decodes the small kjv.txt
-    source once (synth.load_source), which is not the measured workload."""
-    m = max(vals)
-    return [v for v in vals if v > 0.5 * m]
-
-
-def counters(sub):
-    """{counter: [value per bench-sized k_decode dispatch]} (summed over the
-    per-dimension rows rocprofv3 writes for one dispatch)"""
-    per = {}
-    for r in rows(find(sub, "*counter_collection.csv")):
-        if KERNEL not in r.get("Kernel_Name", ""):
-            continue
-        key = (r["Counter_Name"], r.get("Dispatch_Id", ""))
-        per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
-    out = {}
-    for (name, _), v in per.items():
-        out.setdefault(name, []).append(v)
-    sizes = out.get("SQ_WAVE_CYCLES") or out.get("FETCH_SIZE") or out.get("WRITE_SIZE")
-    if sizes:
-        keep = [i for i, v in enumerate(sizes) if v > 0.5 * max(sizes)]
-        out = {k: [v[i] for i in keep] for k, v in out.items()}
-    return out
+def csvs(prof, sub, pat):
+    return glob.glob(os.path.join(prof, sub, "**", pat), recursive=True)
 
 
 def main():
-    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r02"
     workload = sys.argv[2] if len(sys.argv) > 2 else "synthetic 1024 MiB/GPU kjv-tiled .huff"
-    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    stats = find("kt", "*kernel_stats.csv")
-    shutil.copy(stats, os.path.join(ROOT, "profiles", f"{tag}_kernel_stats.csv"))
-    kt = [r for r in rows(find("kt", "*kernel_trace.csv")) if KERNEL in r["Kernel_Name"]]
-    dur = big([(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6 for r in kt])
-    fetch = counters("fetch").get("FETCH_SIZE", [])
-    write = counters("write").get("WRITE_SIZE", [])
-    sq = {k: statistics.mean(v) for k, v in counters("sq").items()}
-    res = {"workload": workload, "kernel": KERNEL, "dispatches": len(dur),
-           "ms_mean": statistics.mean(dur), "ms_min": min(dur), "ms_max": max(dur)}
-    if fetch and write:
-        fb = statistics.mean(fetch) * 1024 * 2
-        wb = statistics.mean(write) * 1024
-        res.update({"fetch_bytes_corrected": fb, "write_bytes": wb,
-                    "hbm_bytes_per_decode": fb + wb,
-                    "fetch_size_kib_raw": statistics.mean(fetch),
-                    "write_size_kib_raw": statistics.mean(write)})
-    res["sq"] = sq
-    with open(os.path.join(ROOT, "profiles", f"{tag}_k_decode.json"), "w") as f:
-        json.dump(res, f, indent=1)
-    if "hbm_bytes_per_decode" in res:
-        with open(os.path.join(ROOT, "profiles", "pmc_latest.json"), "w") as f:
-            json.dump({"workload": workload, "hbm_bytes_per_decode": res["hbm_bytes_per_decode"],
-                       "source": f"profiles/{tag}_k_decode.json"}, f, indent=1)
-    print(json.dumps(res, indent=1))
+    prof = os.path.join(ROOT, "gpurun_out", "prof", tag)
+    out_dir = os.path.join(ROOT, "profiles")
+    stats = csvs(prof, "kt", "*kernel_stats.csv")
+    if stats:
+        shutil.copy(stats[0], os.path.join(out_dir, f"{tag}_kernel_stats.csv"))
+    # durations per dispatch
+    dur = {}
+    for path in csvs(prof, "kt", "*kernel_trace.csv"):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                k = kname(r["Kernel_Name"])
+                if k:
+                    dur.setdefault(k, []).append(
+                        (int(r["Dispatch_Id"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6))
+    res = {"tag": tag, "workload": workload, "kernels": {}}
+    for k, v in dur.items():
+        big = max(d for _, d in v)
+        keep = [d for _, d in v if d >= 0.5 * big]
+        res["kernels"][k] = {"dispatches": len(keep), "ms_mean": round(statistics.mean(keep), 4),
+                             "ms_min": round(min(keep), 4), "ms_max": round(max(keep), 4)}
+    # counters: per kernel, the values of the bench-sized dispatches
+    for sub in ("fetch", "write", "sq1", "sq2"):
+        per = {}
+        for path in csvs(prof, sub, "*counter_collection.csv"):
+            with open(path) as f:
+                for r in csv.DictReader(f):
+                    k = kname(r.get("Kernel_Name", ""))
+                    if not k:
+                        continue
+                    key = (k, r["Counter_Name"], path, r.get("Dispatch_Id", ""))
+                    per[key] = per.get(key, 0.0) + float(r["Counter_Value"])
+        by = {}
+        for (k, name, _, _), v in per.items():
+            by.setdefault((k, name), []).append(v)
+        for (k, name), vs in by.items():
+            top = max(vs)
+            keep = [x for x in vs if x >= 0.5 * top] or vs
+            res["kernels"].setdefault(k, {})[name] = statistics.mean(keep)
+    tot_bytes = 0.0
+    for k, d in res["kernels"].items():
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_bytes"] = 1024.0 * (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"])
+            tot_bytes += d["hbm_bytes"]
+        if "SQ_WAVE_CYCLES" in d and d["SQ_WAVE_CYCLES"]:
+            d["wait_frac"] = round(d.get("SQ_WAIT_ANY", 0) / d["SQ_WAVE_CYCLES"], 3)
+            d["active_frac"] = round(d.get("SQ_ACTIVE_INST_ANY", 0) / d["SQ_WAVE_CYCLES"], 3)
+    res["hbm_bytes_per_decode"] = tot_bytes or None
+    with open(os.path.join(out_dir, f"{tag}_kernels.json"), "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+    if tot_bytes:
+        with open(os.path.join(out_dir, "pmc_latest.json"), "w") as f:
+            json.dump({"workload": workload, "tag": tag, "hbm_bytes_per_decode": tot_bytes,
+                       "per_kernel": {k: d.get("hbm_bytes") for k, d in res["kernels"].items()}},
+                      f, indent=1)
+    print(json.dumps(res, indent=1, sort_keys=True))
 
 
 if __name__ == "__main__":
