@@ -116,6 +116,7 @@ _SIGS = {
     "hh_stage_pipeline": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_uint64,
                            C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
     "hipHuffApproach": ([C.c_void_p, C.c_void_p, C.c_void_p], None),
+    "hh_debug_counters": ([C.c_void_p, C.c_void_p], C.c_int),
 }
 
 
@@ -134,6 +135,8 @@ def lib() -> C.CDLL:
             raise ImportError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
         for name, (args, res) in _SIGS.items():
+            if name.startswith("hh_debug_") and not hasattr(L, name):
+                continue                              # (diagnostics; older A/B builds lack them)
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res

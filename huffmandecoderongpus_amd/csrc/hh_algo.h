@@ -113,6 +113,9 @@ typedef struct {
     uint32_t bt;          /* end of stream relative to the tile (clamped) */
     uint32_t maxadv;      /* most bits one table step advances:
                              max(HH_P, longest code), <= 32             */
+    uint32_t G;           /* overlap: region r's chain starts G bits before
+                             the region (r > 0 within a tile), 0 or a
+                             multiple of 32 <= 64 (see hh_region_head)   */
 } hh_ctx;
 
 /* The kernel is instantiated per words-per-region (the kernel's hh_ctx has
@@ -317,6 +320,38 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
     return u.p < c->bt ? u.p : c->bt;
 }
 
+/* Overlap (c->G > 0).  Region r's chain C_r starts G bits before the
+ * region, at s = R - G, so that it has usually merged with its left
+ * neighbour's chain before the region starts: the head decode runs from s
+ * to y, C_r's first boundary at or past R, and records C_r's boundaries in
+ * [s, R) as bits of *head (bit i <=> a symbol starts at s + i).  Pass 1 then
+ * counts C_r from y, exactly as a chain started at y (so counts, masks and
+ * walks keep the offset-0 semantics with R's entry point y instead of R). */
+HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, uint64_t *head) {
+    uint64_t h = 0;
+    hh_cur u = hh_cur_at(c, s);
+    while (u.p < R && u.p < c->bt) {
+        hh_look L = hh_lookup_w(c, u.p, hh_cur_win(u));
+        const uint32_t o = hh_first_ge(L, R - u.p);     /* first start >= R, or nb */
+        h |= (uint64_t)(L.bm & hh_lowmask(o)) << (u.p - s);
+        hh_cur_adv(c, u, o);
+    }
+    if (head) *head = h;
+    return u.p < c->bt ? u.p : c->bt;
+}
+
+/* The left chain C_j and the right chain C_{j+1} share a boundary in the
+ * overlap window [R - G, R) (R = the start of region j+1) iff C_j's mask
+ * bits there meet C_{j+1}'s head bits: then the chains are identical from
+ * that boundary on, C_j's exit is C_{j+1}'s entry point y, and the walk
+ * from C_j's exit merges at once (k = 1, delta = 0). */
+HH_HD bool hh_window_merge(const hh_ctx *c, const uint32_t *mask, uint64_t head_next, uint32_t R) {
+    uint64_t mine = 0;
+    for (uint32_t w = 0; w < c->G / 32; w++)
+        mine |= (uint64_t)mask[hh_idx(c, (R - c->G) / 32 + w + 2)] << (32 * w);
+    return (mine & head_next) != 0;
+}
+
 /* Symbols of a region's own chain that start before region offset off
  * (popcount of its mask below off). */
 HH_HD uint32_t hh_mask_rank(const hh_ctx *c, const uint32_t *mask, uint32_t R, uint32_t off) {
@@ -349,12 +384,15 @@ HH_HD uint32_t hh_mask_rank(const hh_ctx *c, const uint32_t *mask, uint32_t R, u
 typedef struct {
     uint32_t k, e, cov;
     int32_t delta;
+    uint32_t more;   /* 1: stopped after maxit steps, not finished (k == 0) */
+    uint32_t steps;  /* table lookups the walk took */
 } hh_wk;
 
 HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
                     const uint32_t *mask = nullptr, const uint32_t *xs = nullptr,
-                    const uint16_t *ns = nullptr, uint32_t nmask = 0) {
-    hh_wk r = {0u, 0u, 0u, 0};
+                    const uint16_t *ns = nullptr, uint32_t nmask = 0,
+                    uint32_t maxit = HH_WALK_MAX) {
+    hh_wk r = {0u, 0u, 0u, 0, 0u, 0u};
     const uint32_t bt = c->bt;
     uint32_t A = x < bt ? x : bt;
     int32_t ca = 0;
@@ -377,7 +415,7 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
                 mh = mask[hh_idx_next(c, u.a)];
                 cur_ok = true;
             }
-            for (; u.p < Ec && it < HH_WALK_MAX; it++) {
+            for (; u.p < Ec && it < maxit; it++) {
                 const uint32_t win = hh_cur_win(u);
                 const uint32_t m = c->l1m[win & (HH_L1_SIZE - 1u)];
                 uint32_t lns = HH_M_NSYM(m), lnb = HH_M_NBITS(m), lbm = HH_M_BMASK(m);
@@ -395,6 +433,7 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
                     r.e = e;
                     r.cov = (uint32_t)ca0;
                     r.delta = (ca - ca0) - (int32_t)hh_mask_rank(c, mask, R, u.p - R + t);
+                    r.steps = it + 1;
                     return r;
                 }
                 uint32_t adv = lnb;
@@ -417,17 +456,22 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
                 r.e = e;
                 r.cov = (uint32_t)ca0;
                 r.delta = (ca - ca0) - (int32_t)ns[rg];
+                r.steps = it;
                 return r;
             }
         } else {
+            /* the region's own chain, entered at its entry point: the
+             * next tile's region 0 starts at R, the others G bits early */
             uint32_t B = R < bt ? R : bt;
+            if (c->G && rg > nmask && R < bt) B = hh_region_head(c, R - c->G, R, nullptr);
             int32_t cb = 0;
-            for (; it < HH_WALK_MAX; it++) {
+            for (; it < maxit; it++) {
                 if (A == B) {
                     r.k = k;
                     r.e = e;
                     r.cov = (uint32_t)ca0;
                     r.delta = (ca - ca0) - cb;
+                    r.steps = it;
                     return r;
                 }
                 const bool mvA = A < B;
@@ -442,9 +486,11 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
                 if (mvA) { A = np; ca += n; } else { B = np; cb += n; }
             }
         }
-        if (it >= HH_WALK_MAX) break;
+        if (it >= maxit) break;
     }
-    return r;   /* k == 0: failed */
+    r.more = it >= maxit && maxit < HH_WALK_MAX;
+    r.steps = it;
+    return r;   /* k == 0: failed (or, with more, not finished yet) */
 }
 
 /* ------------------------------------------------------------------ */
@@ -526,6 +572,15 @@ HH_HD uint32_t hh_inc_state(uint64_t g) { return (uint32_t)(g >> 40) & 0x1fffffu
 /* the prefix, sign-extended (a segment's virtual predecessor carries the
  * entry correction, which may be negative) */
 HH_HD uint64_t hh_inc_prefix(uint64_t g) { return (uint64_t)((int64_t)(g << 24) >> 24); }
+
+/* Overlap G for a tree (hh_region_head): 64 bits when that keeps chain
+ * starts on the code-length lattice (a multiple of the length gcd); none
+ * for a fixed-length code (its chains sit on one lattice and merge at
+ * once). */
+HH_HD uint32_t hh_pick_overlap(const hh_tables *t) {
+    const uint32_t g = t->len_gcd > 0 ? (uint32_t)t->len_gcd : 1u;
+    return t->fixed_len > 0 || 64u % g ? 0u : 64u;
+}
 
 /* Region size for a code whose lengths are all multiples of g: a multiple
  * of 32 (whole words per region column) and of g (region starts on the

@@ -61,7 +61,10 @@ struct DevTab {
     const uint32_t *tree;
     const uint8_t *tsym;
     uint32_t l2_used;
+    uint32_t tree_lds;   // compact tree nodes k_emit stages in LDS
 };
+#define HH_TREE_LDS_MAX 1024   // nodes: a byte alphabet's tree has <= 511 unless symbols repeat;
+                               // larger trees take the stage pipeline
 
 // flags[0]: status bits; [2..3] total symbols (u64); [4..9] first failed walk;
 // [12] a prologue tile is CONST; [13] an emitted tile is CONST; [14] state
@@ -87,6 +90,7 @@ struct Geometry {
     uint32_t S, sw;
     uint32_t vec4;       // 16-B aligned payload and sw % 4 == 0
     uint32_t maxadv;     // max(HH_P, longest code)
+    uint32_t G;          // overlap bits (hh_region_head)
     uint32_t in_state;   // state entering tile 0 (a shard's entry; 0 at the stream start)
     uint64_t emit_from;  // tiles before this one are a prologue: decoded for their
                          // leaving state only (a shard's probe of its predecessor)
@@ -239,10 +243,27 @@ __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, 
 }
 
 #ifndef HH_FRONT_MINW
-#define HH_FRONT_MINW 4   // waves per SIMD the front kernel's registers are sized for
+#define HH_FRONT_MINW 5   // waves per SIMD the front kernel's registers are sized for (<= 96
+                          // VGPRs; its LDS also admits 5 workgroups per CU)
 #endif
 #ifndef HH_EMIT_MINW
 #define HH_EMIT_MINW 4
+#endif
+
+// Diagnostic build only (-DHH_DIAG): wave 0 of every workgroup stamps the
+// shader clock between the front kernel's phases and adds the cycles into
+// dbg[phase]; walk statistics go to dbg[8..]: lanes, lookups, the sum over
+// tiles of the longest walk, the longest walk.  hh_debug_counters reads them.
+#ifdef HH_DIAG
+#define DIAG_DECL uint64_t dg_acc[6] = {0, 0, 0, 0, 0, 0}, dg_w[4] = {0, 0, 0, 0}; uint64_t dg_t = __builtin_amdgcn_s_memtime();
+#define DIAG_STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); dg_acc[i] += t_ - dg_t; dg_t = t_; } while (0)
+#define DIAG_FLUSH(dbg) do { if (threadIdx.x == 0) for (int i_ = 0; i_ < 6; i_++) atomicAdd((unsigned long long *)&(dbg)[i_], (unsigned long long)dg_acc[i_]); \
+    if ((threadIdx.x & 63u) == 0) { for (int i_ = 0; i_ < 3; i_++) atomicAdd((unsigned long long *)&(dbg)[8 + i_], (unsigned long long)dg_w[i_]); \
+        atomicMax((unsigned long long *)&(dbg)[11], (unsigned long long)dg_w[3]); } } while (0)
+#else
+#define DIAG_DECL
+#define DIAG_STAMP(i) do {} while (0)
+#define DIAG_FLUSH(dbg) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -250,7 +271,7 @@ __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, 
 // ---------------------------------------------------------------------------
 template <uint32_t SW>
 __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *__restrict__ gdata, Geometry geo,
-                                                                 DevTab tab, Work wk) {
+                                                                 DevTab tab, Work wk, uint64_t *dbg) {
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ uint32_t s_x[HH_NR];            // pass-1 exits
     __shared__ uint16_t s_n[HH_NR];            // pass-1 counts
@@ -283,10 +304,12 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
     c.tree = tab.tree;
     c.tsym = tab.tsym;
     c.maxadv = geo.maxadv;
+    c.G = geo.G;
 
     Prefetch pf;
     uint64_t t = blockIdx.x;
     if (t < geo.ntiles) prefetch_tile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords, geo.vec4);
+    DIAG_DECL
     for (; t < geo.ntiles; t += gridDim.x) {
         __syncthreads();                                // previous tile's LDS no longer read
         const uint64_t rem = geo.bits - t * tile_bits;
@@ -296,26 +319,63 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
         const uint64_t tn = t + gridDim.x;
         if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
         __syncthreads();
+        DIAG_STAMP(0);
 
         // pass 1: own region from offset 0
+        // pass 1: the head (from G bits before the region, lanes > 0), then
+        // the own chain from its entry point y, counted and masked
         const uint32_t p0 = j * S;
         uint32_t n = 0, x = bt;
+        uint64_t head = 0;
         if (p0 < bt) {
+            const uint32_t y = j > 0 && c.G ? hh_region_head(&c, p0 - c.G, p0, &head) : p0;
             const uint32_t lim = p0 + S < bt ? p0 + S : bt;
-            x = hh_region_count(&c, p0, lim, &n, s_mk);
+            x = y < lim ? hh_region_count(&c, y, lim, &n, s_mk) : y;
         }
         s_x[j] = x;
         s_n[j] = (uint16_t)n;
         __syncthreads();
+        DIAG_STAMP(1);
+        // region j+1's chain met this one in the overlap window: merged at
+        // this chain's exit, no walk.  Its head comes from the next lane of
+        // the wave; the last lane of a wave walks (one lookup when merged).
+        const uint32_t R1 = (j + 1) * S;
+        const uint32_t hlo = (uint32_t)__shfl_down((int)(uint32_t)head, 1, 64);
+        const uint32_t hhi = (uint32_t)__shfl_down((int)(uint32_t)(head >> 32), 1, 64);
+        const bool merged = c.G && (j & 63u) != 63u && R1 < bt &&
+                            hh_window_merge(&c, s_mk, ((uint64_t)hhi << 32) | hlo, R1);
 
         // walks: region j's exit against the next regions' own chains
-        const hh_wk w = hh_walk(&c, j, S, x, s_mk, s_x, s_n, HH_NR);
+#ifndef HH_EXP_NOWALK
+        hh_wk w = {1u, x - R1, 0u, 0, 0u, 0u};
+        if (!merged) w = hh_walk(&c, j, S, x, s_mk, s_x, s_n, HH_NR);
+#else
+        const hh_wk w = {1u, 0u, 0u, 0, 0u, 0u};
+#endif
         if (w.k == 0) {
             atomicOr(wk.flags, (uint32_t)F_FAIL);
             if (atomicCAS(&wk.flags[4], 0u, 1u) == 0u) {
                 wk.flags[5] = (uint32_t)t; wk.flags[6] = j; wk.flags[7] = x; wk.flags[8] = n; wk.flags[9] = bt;
             }
         }
+#ifdef HH_DIAG
+        {
+            const uint32_t st = w.steps;
+            uint32_t mx = st;
+            uint64_t sm = st;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+                sm += (uint32_t)__shfl_xor((int)(uint32_t)sm, o, 64);
+            }
+            dg_w[0] += 64;
+            dg_w[1] += sm;
+            dg_w[2] += mx;                               // per wave
+            dg_w[3] = dg_w[3] > mx ? dg_w[3] : mx;
+        }
+        __syncthreads();
+        DIAG_STAMP(2);
+#endif
         const uint32_t kk = w.k ? w.k : 1u;
         if (j < HH_KM) s_cd[j] = 0;
         resolve_live(kk, s_k, s_mem, s_exc, s_cnt);     // barriers inside
@@ -352,7 +412,9 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
             if (j < HH_KM)
                 wk.tabs[t * HH_KM + j] = hh_tab_pack(cnt, os) | (j == 0 && cst ? HH_CST : 0ull);
         }
+        DIAG_STAMP(3);
     }
+    DIAG_FLUSH(dbg);
 }
 
 // ---------------------------------------------------------------------------
@@ -464,11 +526,19 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     uint32_t *s_w = s_l1s + HH_L1_SIZE;                 // SW * HH_NLS words (transposed)
     uint32_t *s_out = s_w + SW * HH_NLS;                // HH_OB bytes of output staging
     uint32_t *s_l2 = s_out + HH_OB / 4;
+    uint32_t *s_tree = s_l2 + tab.l2_used;              // the compact tree (tail rule, long codes)
+    uint8_t *s_tsym = (uint8_t *)(s_tree + tab.tree_lds);
 
     const uint32_t j = threadIdx.x;
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
     const uint32_t span = HH_NCOL * S;
     load_tables(tab, s_l1m, s_l1s, s_l2);
+    // with the tree in LDS too, the decode loops issue no global load: a
+    // global load there would make them wait for the next tile's prefetch
+    for (uint32_t i = j; i < tab.tree_lds; i += HH_NL) {
+        s_tree[i] = tab.tree[i];
+        s_tsym[i] = tab.tsym[i];
+    }
 
     hh_ctx c;
     c.w = s_w;
@@ -477,28 +547,57 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     c.l1m = s_l1m;
     c.l1s = s_l1s;
     c.l2 = s_l2;
-    c.tree = tab.tree;
-    c.tsym = tab.tsym;
+    c.tree = s_tree;                                    // (fast_path_ok: the tree fits)
+    c.tsym = s_tsym;
     c.maxadv = geo.maxadv;
+    c.G = geo.G;
 
+    // the next tile's words, lane record, entering state and output base are
+    // loaded one tile ahead (they are the loads every phase below waits on)
     Prefetch pf;
+    uint32_t rec_n = 0, meta_n = 0;
+    // Issued BEFORE the words (vmcnt retires in order: consuming them then
+    // does not wait for the words).  The tile's entering state and output
+    // base are uniform, but a uniform load is moved to an SGPR -- and waited
+    // for -- at once; so lanes 0..3 of every wave load one word each (state, base low,
+    // base high, block-local prefix) and the words are read out of lanes
+    // 0..3 only where the next tile consumes them.
+    auto prefetch_meta = [&](uint64_t tt) {
+        rec_n = wk.recs[tt * HH_NR + j];
+        const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / HH_SCAN_TB);
+        const uint32_t ln = j & 63u;                    // (every wave reads its own copy)
+        const uint32_t *src = ln == 0 ? &wk.st[tt] : ln == 1 ? blk32 : ln == 2 ? blk32 + 1
+                                                                   : (const uint32_t *)&wk.lex[tt];
+        meta_n = *src;
+    };
     uint64_t t = geo.emit_from + blockIdx.x;
-    if (t < geo.ntiles) prefetch_tile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords, geo.vec4);
+    if (t < geo.ntiles) {
+        prefetch_meta(t);
+        prefetch_tile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords, geo.vec4);
+    }
     for (; t < geo.ntiles; t += gridDim.x) {
         __syncthreads();                                // previous tile's LDS no longer read
         const uint64_t rem = geo.bits - t * tile_bits;
         c.bt = rem < span ? (uint32_t)rem : span;
         const uint32_t bt = c.bt;
         store_tile<SW>(pf, s_w);
+        const uint32_t rec = rec_n;
+        // (readlane returns int: every word is cast to uint32_t before widening)
+        const uint32_t st_in = (uint32_t)__builtin_amdgcn_readlane(meta_n, 0);
+        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane(meta_n, 1);
+        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane(meta_n, 2);
+        const int32_t lex_t = __builtin_amdgcn_readlane(meta_n, 3);
+        const int64_t base_t = (int64_t)(((uint64_t)bhi << 32) | blo) + (int64_t)lex_t;
         const uint64_t tn = t + gridDim.x;
-        if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
-        const uint32_t rec = wk.recs[t * HH_NR + j];
+        if (tn < geo.ntiles) {
+            prefetch_meta(tn);
+            prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
+        }
         const uint32_t kk = rec_k(rec), ee = rec_e(rec);
         const int32_t dl = rec_delta(rec);
         resolve_live(kk, s_k, s_mem, s_exc, s_cnt);     // barriers inside (also publish s_w)
 
         // the entering state: first live lane d_t, entered e_t bits in
-        const uint32_t st_in = wk.st[t];
         const uint32_t d_t = hh_state_d(st_in);
         const int32_t dprev = hh_state_delta(st_in);
         const bool live = (s_mem[j] >> d_t) & 1u;
@@ -513,11 +612,17 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
         int32_t Tout_i;
         const uint32_t L = (uint32_t)block_excl_scan<HH_NL>((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
         const uint32_t Tout = (uint32_t)Tout_i;
-        const int64_t P0s = wk.blk[t / HH_SCAN_TB] + (int64_t)wk.lex[t] - (int64_t)dprev;
+        const int64_t P0s = base_t - (int64_t)dprev;
         const uint64_t P0 = (uint64_t)P0s;
         // the tile's output fits [0, cap) (no wrap-around)
         const bool fits = P0s >= 0 && P0 <= cap && Tout <= cap - P0;
         if (j == 0 && !fits) atomicOr(wk.flags, (uint32_t)F_OVER);
+#ifdef HH_DEBUG_OVER
+        if (j == 0 && !fits && atomicAdd(&wk.flags[4], 1u) == 0) {
+            wk.flags[5] = (uint32_t)t; wk.flags[6] = (uint32_t)P0; wk.flags[7] = (uint32_t)(P0 >> 32);
+            wk.flags[8] = Tout; wk.flags[9] = st_in;
+        }
+#endif
 
         hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
         const uint32_t y = (j + kk) * S + ee;
@@ -536,7 +641,11 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
             const uint32_t nq = (a0 + Tout + 15u) / 16u;
             for (uint32_t i = j; i < nq; i += HH_NL) *(u32x4 *)(s_out + 4 * i) = (u32x4){0u, 0u, 0u, 0u};
             __syncthreads();
+#ifdef HH_EXP_NODEC
+            if (false) {
+#else
             if (cu.p < pe) {
+#endif
                 const uint32_t b = a0 + L;
                 uint32_t wd = b >> 2, nacc = b & 3u, emitted = 0, val, k;
                 uint64_t acc = 0;
@@ -581,7 +690,11 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
             for (uint32_t i = j; i < nq; i += HH_NL) {
                 const uint32_t lo = 16 * i;
                 if (lo >= a0 && lo + 16 <= a0 + Tout) {
+#ifdef HH_EXP_NT
                     __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
+#else
+                    *(u32x4 *)(gb + lo) = *(const u32x4 *)(sb + lo);
+#endif
                 } else {                           // a block shared with a neighbouring tile
                     const uint32_t e = lo + 16 < a0 + Tout ? lo + 16 : a0 + Tout;
                     for (uint32_t q = lo > a0 ? lo : a0; q < e; q++) gb[q] = sb[q];
@@ -726,7 +839,7 @@ __global__ void k_st_findmax(int64_t bits, const int32_t *idx, int32_t *maxv) {
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-typedef void (*kfront_t)(const uint32_t *, Geometry, DevTab, Work);
+typedef void (*kfront_t)(const uint32_t *, Geometry, DevTab, Work, uint64_t *);
 typedef void (*kemit_t)(const uint32_t *, Geometry, DevTab, Work, uint8_t *, uint64_t);
 
 struct hh_decoder {
@@ -741,16 +854,19 @@ struct hh_decoder {
     uint8_t *d_tsym;
     DevTab tab;
     uint32_t S;
+    uint32_t G;          // overlap bits (hh_pick_overlap; HH_OVERLAP overrides)
     // workspace
     void *ws;
     size_t ws_size;
     uint32_t *h_flags;   // pinned
     int32_t *d_max;      // findmax result (stage API)
+    uint64_t *d_dbg;     // HH_DIAG counters (16 x u64)
     hipEvent_t ev[4];
     hh_stats stats;
     uint32_t grid_f, grid_e;   // persistent grid sizes (occupancy x CUs)
     uint32_t grid_sw;          // words per region they were sized for
     size_t grid_l2;            // and the L2 table size
+    uint32_t grid_tree;        // and the LDS tree size
     // host staging of the evaluate() scope (hh_decode_host)
     uint8_t *h_stage;
     size_t h_stage_size;
@@ -790,6 +906,7 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
         hipMalloc(&d->d_tree, sizeof(uint32_t) * (HH_TREE_MAX + 1)) != hipSuccess ||
         hipMalloc(&d->d_tsym, HH_TREE_MAX + 1) != hipSuccess ||
         hipMalloc(&d->d_max, 16) != hipSuccess ||
+        hipMalloc(&d->d_dbg, 16 * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc((void **)&d->h_flags, 64, hipHostMallocDefault) != hipSuccess) {
         hh_decoder_destroy(d);
         return HH_ERR_DEVICE;
@@ -813,6 +930,7 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
     if (d->d_tree) hipFree(d->d_tree);
     if (d->d_tsym) hipFree(d->d_tsym);
     if (d->d_max) hipFree(d->d_max);
+    if (d->d_dbg) hipFree(d->d_dbg);
     if (d->d_in) hipFree(d->d_in);
     if (d->d_out) hipFree(d->d_out);
     if (d->h_stage) hipHostFree(d->h_stage);
@@ -859,7 +977,11 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     d->tab.tree = d->d_tree;
     d->tab.tsym = d->d_tsym;
     d->tab.l2_used = d->ht->l2_used;
+    d->tab.tree_lds = d->ht->tree_used;
     d->S = pick_region_bits(d->ht, d->cfg.lane_bits);
+    d->G = hh_pick_overlap(d->ht);
+    if (getenv("HH_OVERLAP")) d->G = (uint32_t)atoi(getenv("HH_OVERLAP")) & ~31u;   // experiments
+    if (d->G > 64 || d->G + 32 > d->S) d->G = 0;
     d->have_tree = 1;
     return HH_OK;
 }
@@ -879,7 +1001,7 @@ static inline unsigned grid_for(int64_t n, unsigned bs) {
 
 static int fast_path_ok(const hh_decoder *d) {
     return d->S >= 32 && d->S <= 32 * HH_SW_MAX && d->ht->maxlen <= HH_MAXLEN_FAST &&
-           !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
+           d->ht->tree_used <= HH_TREE_LDS_MAX && !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
 }
 
 static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8_t *d_out,
@@ -888,8 +1010,8 @@ static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8
 static size_t lds_front(uint32_t sw, uint32_t l2) {
     return ((size_t)HH_L1_SIZE + 2 * (size_t)sw * HH_NLS + l2) * 4;
 }
-static size_t lds_emit(uint32_t sw, uint32_t l2) {
-    return (2 * (size_t)HH_L1_SIZE + (size_t)sw * HH_NLS + l2) * 4 + HH_OB;
+static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree) {
+    return (2 * (size_t)HH_L1_SIZE + (size_t)sw * HH_NLS + l2) * 4 + HH_OB + (size_t)tree * 5;
 }
 
 // kernels instantiated per words-per-region (S = 32 * SW bits)
@@ -913,16 +1035,18 @@ static kemit_t kemit_for(uint32_t sw) {
 
 // Persistent grids: the occupancy answer x CUs for each kernel.
 static int size_grids(hh_decoder *d, uint32_t sw) {
-    if (d->grid_f && d->grid_sw == sw && d->grid_l2 == d->tab.l2_used) return HH_OK;
+    if (d->grid_f && d->grid_sw == sw && d->grid_l2 == d->tab.l2_used && d->grid_tree == d->tab.tree_lds)
+        return HH_OK;
     int pf = 0, pe = 0, ncu = 0;
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pf, kfront_for(sw), HH_NL, lds_front(sw, d->tab.l2_used)));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kemit_for(sw), HH_NL, lds_emit(sw, d->tab.l2_used)));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kemit_for(sw), HH_NL, lds_emit(sw, d->tab.l2_used, d->tab.tree_lds)));
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
     if (pf < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
     d->grid_f = (uint32_t)(pf * ncu);
     d->grid_e = (uint32_t)(pe * ncu);
     d->grid_sw = sw;
     d->grid_l2 = d->tab.l2_used;
+    d->grid_tree = d->tab.tree_lds;
     return HH_OK;
 }
 
@@ -992,6 +1116,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     geo.S = d->S;
     geo.sw = d->S / 32;
     geo.maxadv = d->ht->maxlen > HH_P ? (uint32_t)d->ht->maxlen : HH_P;
+    geo.G = d->G;
     geo.nwords = ((bits_avail + 7) / 8 + HH_PAYLOAD_PAD) / 4;
     geo.in_state = in_state;
     geo.emit_from = emit_from;
@@ -1025,9 +1150,12 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     const uint32_t ge = (uint32_t)(ne < d->grid_e ? (ne ? ne : 1) : d->grid_e);
 
     HIP_OK(hipMemsetAsync(wk.flags, 0, 64, st));
+#ifdef HH_DIAG
+    HIP_OK(hipMemsetAsync(d->d_dbg, 0, 16 * sizeof(uint64_t), st));
+#endif
     HIP_OK(hipEventRecord(d->ev[0], st));
     hipLaunchKernelGGL(kf, dim3(gf), dim3(HH_NL), lds_front(geo.sw, d->tab.l2_used), st,
-                       (const uint32_t *)d_data, geo, d->tab, wk);
+                       (const uint32_t *)d_data, geo, d->tab, wk, d->d_dbg);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d->ev[1], st));
     hipLaunchKernelGGL(k_scan1, dim3(nblk), dim3(HH_SCAN_TB), 0, st, geo, wk);
@@ -1036,7 +1164,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d->ev[2], st));
     if (ne) {
-        hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used), st,
+        hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds), st,
                            (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap);
         HIP_OK(hipGetLastError());
     }
@@ -1048,7 +1176,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
         rc = scan_host(d, geo, wk, nblk, st);
         if (rc) return rc;
         if (ne) {
-            hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used), st,
+            hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds), st,
                                (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap);
             HIP_OK(hipGetLastError());
         }
@@ -1318,4 +1446,15 @@ extern "C" int hh_debug_failure(hh_decoder *d, uint32_t *out5) {
     if (hipMemcpy(f, d->ws, sizeof(f), hipMemcpyDeviceToHost) != hipSuccess) return HH_ERR_DEVICE;
     for (int i = 0; i < 5; i++) out5[i] = f[5 + i];
     return (int)f[4];
+}
+
+// Diagnostic (HH_DIAG builds; zeros otherwise): the front kernel's phase
+// cycles summed over workgroups [0..3] (staging, pass 1, walks, table) and
+// walk statistics [8..11] (lanes, lookups, sum over waves of the wave's
+// longest walk, longest walk) of the last decode.
+extern "C" int hh_debug_counters(hh_decoder *d, uint64_t *out16) {
+    if (!d || !out16) return HH_ERR_ARG;
+    if (hipMemcpy(out16, d->d_dbg, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return HH_ERR_DEVICE;
+    return HH_OK;
 }

@@ -47,6 +47,8 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
     for (int i = 0; i < 8; i++) stats[i] = 0;
     if (S == 0) S = hh_pick_region_bits((uint32_t)T.len_gcd);
     stats[3] = S;
+    uint32_t G = hh_pick_overlap(&T);
+    if (getenv("HH_EMU_G")) G = (uint32_t)atoi(getenv("HH_EMU_G"));
     if (leave) *leave = in_state;
     if (entry) *entry = in_state;
     if (bits == 0) return 0;
@@ -66,6 +68,7 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
         l1s[i] = (uint32_t)T.l1[i];
     }
     std::vector<uint32_t> mk((size_t)sw * HH_NLS);   // boundary masks (transposed like w)
+    std::vector<uint64_t> hd(HH_NR);                 // overlap heads (hh_region_head)
     std::vector<int32_t> din(HH_NR);
     std::vector<hh_wk> wk(HH_NR);
     stats[0] = (int64_t)ntiles;
@@ -98,23 +101,31 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
         c.tree = T.tree;
         c.tsym = T.tsym;
         c.maxadv = T.maxlen > HH_P ? (uint32_t)T.maxlen : HH_P;
+        c.G = G;
         const uint64_t rem = bits - t * TB;
         c.bt = rem < span ? (uint32_t)rem : span;
         const uint32_t bt = c.bt;
 
         for (size_t i = 0; i < mk.size(); i++)          // words pass 1 leaves unwritten
             mk[i] = (uint32_t)(0x9e3779b9u * (uint32_t)(i + t * 7919u + 1));   // hold junk
-        for (uint32_t j = 0; j < HH_NR; j++) {            // pass 1
-            uint32_t p0 = j * S, n = 0, x = bt;
+        for (uint32_t j = 0; j < HH_NR; j++) {            // pass 1 (head, then count)
+            uint32_t p0 = j * S, n = 0, x = bt, y = p0;
+            hd[j] = 0;
             if (p0 < bt) {
+                if (j > 0 && G) y = hh_region_head(&c, p0 - G, p0, &hd[j]);
                 uint32_t lim = p0 + S < bt ? p0 + S : bt;
-                x = hh_region_count(&c, p0, lim, &n, mk.data());
+                x = y < lim ? hh_region_count(&c, y, lim, &n, mk.data()) : y;
             }
             xs[j] = x;
             ns[j] = n;
             n16[j] = (uint16_t)n;
         }
-        for (uint32_t j = 0; j < HH_NR; j++) {            // walks
+        for (uint32_t j = 0; j < HH_NR; j++) {            // window checks, else walks
+            const uint32_t R1 = (j + 1) * S;
+            if (G && j + 1 < HH_NR && R1 < bt && hh_window_merge(&c, mk.data(), hd[j + 1], R1)) {
+                wk[j] = hh_wk{1u, xs[j] - R1, 0u, 0, 0u, 0u};
+                continue;
+            }
             wk[j] = hh_walk(&c, j, S, xs[j], mk.data(), xs.data(), n16.data(), HH_NR);
             if (wk[j].k == 0) stats[2]++;
             if (wk[j].k > 1) stats[1]++;

@@ -19,7 +19,19 @@ from huffmandecoderongpus_amd import synth  # noqa: E402
 mib = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 src = sys.argv[3] if len(sys.argv) > 3 else "kjv.txt"
-hf, text = synth.load_source(os.path.join(ROOT, "files"), src)
+# the source text comes from the in-tree library (tools/ab.sh caches it), so
+# that an experiment variant under test never decodes its own reference
+cache = os.environ.get("HH_TEXT_CACHE")
+if cache and os.path.exists(cache):
+    import numpy as np
+    hf = H.HuffFile.load(os.path.join(ROOT, "files", src + ".huff"))
+    text = np.load(cache)
+else:
+    hf, text = synth.load_source(os.path.join(ROOT, "files"), src)
+    if cache:
+        import numpy as np
+        np.save(cache, text)
+        sys.exit(0)
 syn = synth.tiled_stream(hf, text, mib << 20)
 dec = H.Decoder(0)
 dec.set_tree(syn.tree)
@@ -27,7 +39,10 @@ out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device="cuda")
 ph = {"total": [], "sync": [], "scan": [], "emit": []}
 ok = True
 for i in range(reps + 1):
-    n = dec.decode_device(syn.data, syn.bits, out)
+    try:
+        n = dec.decode_device(syn.data, syn.bits, out)
+    except H.HipHuffError:          # experiment variants (wrong counts by design)
+        n = -1
     torch.cuda.synchronize()
     if i == 0:
         ok = n == syn.decoded_bytes and synth.verify_tiled(out, syn)
@@ -38,4 +53,14 @@ for i in range(reps + 1):
 res = {"lib": os.path.basename(os.environ.get("HIPHUFF_LIB", H.LIB_PATH)), "mib": mib, "src": src,
        "ok": bool(ok), "fast": dec.stats()["exact_fallback"] == 0}
 res.update({k: round(statistics.median(v), 4) for k, v in ph.items()})
+if os.environ.get("HH_DIAG"):            # a -DHH_DIAG build: phase cycles and walk lengths
+    import ctypes as C
+    buf = (C.c_uint64 * 16)()
+    H.lib().hh_debug_counters(dec._h, buf)
+    cyc = [buf[i] for i in range(4)]
+    tot = sum(cyc) or 1
+    res["front_phase_frac"] = {n: round(v / tot, 3) for n, v in zip(("stage", "pass1", "walks", "table"), cyc)}
+    if buf[8]:
+        res["walk"] = {"mean_steps": round(buf[9] / buf[8], 2), "mean_wave_max": round(buf[10] / (buf[8] / 64), 2),
+                       "max": buf[11]}
 print(json.dumps(res), flush=True)
