@@ -60,7 +60,9 @@ clean:
 
 # A/B variant of the library: make variant V=name HIPEXTRA="-DHH_X=1"
 # -> build/libhiphuff_<name>.so (tools/ab.sh)
-variant: $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
+variant: $(BUILD)/hh_plugin.o
 	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/hh_device.hip -o $(BUILD)/hh_device_$(V).o
-	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/libhiphuff_$(V).so $(BUILD)/hh_device_$(V).o $^
+	$(CC) $(CFLAGS) $(HIPEXTRA) -c $(CSRC)/hh_huff.c -o $(BUILD)/hh_huff_$(V).o
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/libhiphuff_$(V).so $(BUILD)/hh_device_$(V).o \
+	    $(BUILD)/hh_huff_$(V).o $^
 .PHONY: variant

@@ -46,6 +46,8 @@ def _args():
     ap.add_argument("--files", default=os.path.join(ROOT, "files"))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the E.coli / i.i.d. workloads and the evaluate()-scope timing")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="HBM traffic measured by rocprofv3 --pmc (tools/profile.sh)")
     return ap.parse_args()
@@ -95,6 +97,61 @@ def cpu_baseline(files_dir: str, seconds: float) -> dict:
                        f"({D} B decoded), median of {len(times)} runs over ~{seconds:.0f} s, "
                        f"tables built inside each timed call; host {cpu}, "
                        f"nproc {os.cpu_count()}")}
+
+
+def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, steps: int,
+                    warmup: int) -> dict:
+    """One more single-GPU workload, device-resident like the headline one:
+    correctness first, then `steps` timed decodes (kernel time from the
+    decoder's HIP events, wall time around the loop)."""
+    import torch
+    n = dec.decode_device(data, bits, out)
+    torch.cuda.synchronize()
+    ok = n == n_want and verify(out)
+    for _ in range(warmup):
+        dec.decode_device(data, bits, out)
+    torch.cuda.synchronize()
+    st = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dec.decode_device(data, bits, out)
+        st.append(dec.stats())
+    torch.cuda.synchronize()
+    ms_step = (time.perf_counter() - t0) / steps * 1e3
+    ms_dev = statistics.mean(s["ms_total"] for s in st)
+    C = (bits + 7) // 8
+    ach = (C + n_want) / (ms_dev * 1e-3) / 1e9
+    return {"workload": name, "ok": bool(ok), "value": round(n_want / (ms_step * 1e-3) / 1e6, 1),
+            "unit": "MB/s", "ms_per_step": round(ms_step, 4), "ms_kernel": round(ms_dev, 4),
+            "ms_front": round(statistics.mean(s["ms_sync"] for s in st), 4),
+            "ms_emit": round(statistics.mean(s["ms_emit"] for s in st), 4),
+            "compressed_bytes": C, "decoded_bytes": n_want,
+            "roofline_frac": round(ach / HBM_PEAK_GBS, 4),
+            "fast_path": all(s["exact_fallback"] == 0 for s in st)}
+
+
+def evaluate_scope(H, hf, payload, bits: int, n_want: int, reps: int, check=None) -> dict:
+    """The reference's evaluate() scope (decodeUtil.c:41-43: the whole
+    decoder call is timed): host payload in, host symbols out, through
+    hh_decode_host (pinned staging kept by the decoder, chunked copies
+    overlapped with the decode)."""
+    import numpy as np
+    dec = H.Decoder(0)
+    try:
+        dec.set_tree(hf.tree())
+        out = dec.decode_host(payload, bits, n_want + 16)        # first call: allocations
+        ok = len(out) == n_want and (check is None or check(out))
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            out = dec.decode_host(payload, bits, n_want + 16)
+            ts.append(time.perf_counter() - t0)
+        del out
+        ms = statistics.median(ts) * 1e3
+        return {"ok": bool(ok), "ms": round(ms, 3), "MBps": round(n_want / (ms * 1e-3) / 1e6, 1),
+                "decoded_bytes": n_want, "reps": reps}
+    finally:
+        dec.close()
 
 
 def load_pmc(path: str, workload: str):
@@ -251,6 +308,43 @@ def main():
         "fast_path": fast,
     }
     res.update(extra)
+    if world == 1 and not a.no_extra:
+        # SURVEY 8d's other single-GPU configs and the evaluate() scope
+        # (after the headline measurement, outside its timed region)
+        import numpy as np
+        del out
+        torch.cuda.empty_cache()
+        ks = max(3, min(a.steps, 10))
+        more = []
+        hfe, texte = synth.load_source(a.files, "E.coli", device=local)
+        syn_e = synth.tiled_stream(hfe, texte, target, device=dev)
+        dec_e = H.Decoder(local)
+        dec_e.set_tree(syn_e.tree)
+        out_e = torch.empty(syn_e.decoded_bytes + 4096, dtype=torch.uint8, device=dev)
+        more.append(device_workload(f"synthetic {a.size_mib} MiB E.coli-tiled .huff", dec_e,
+                                    syn_e.data, syn_e.bits, out_e, syn_e.decoded_bytes,
+                                    lambda o: synth.verify_tiled(o, syn_e), ks, 2))
+        dec_e.close()
+        del out_e, syn_e
+        torch.cuda.empty_cache()
+        iid = synth.iid_stream(hf, text, target, device=dev)
+        out_i = torch.empty(iid.decoded_bytes + 4096, dtype=torch.uint8, device=dev)
+        more.append(device_workload(f"synthetic {a.size_mib} MiB i.i.d. kjv-unigram .huff "
+                                    f"(splitmix64 seed {synth.IID_SEED:#x})", dec, iid.data,
+                                    iid.bits, out_i, iid.decoded_bytes,
+                                    lambda o: bool(torch.equal(o[:iid.decoded_bytes], iid.syms)),
+                                    ks, 2))
+        del out_i, iid
+        torch.cuda.empty_cache()
+        res["workloads"] = more
+        # evaluate() scope: kjv.txt.huff itself, and the headline 1 GiB stream from host memory
+        ev = {"kjv.txt": evaluate_scope(H, hf, hf.payload, hf.bits, hf.uncompressedsize, 20,
+                                        lambda o: np.array_equal(o, text))}
+        host_pay = syn.data[: syn.compressed_bytes].cpu().numpy()
+        ev[f"{a.size_mib} MiB kjv-tiled"] = evaluate_scope(H, hf, host_pay, syn.bits,
+                                                           syn.decoded_bytes, 3)
+        del host_pay
+        res["evaluate"] = ev
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.files, a.cpu_seconds)
     if rank == 0:

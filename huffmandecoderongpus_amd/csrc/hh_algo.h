@@ -158,6 +158,16 @@ HH_HD uint32_t hh_bit(const hh_ctx *c, uint32_t p) {
 /* The reference's tail rule (decodeallbits.cl:20-31): walking from the root
  * at p, stop at a leaf or at the end of the stream; the node reached gives
  * the symbol byte.  Used only for a code cut off by the end of the stream. */
+/* The tree may live in global memory (k_front): these rare paths end with
+ * an explicit wait, so that their loads are complete where the decode loops
+ * join them again -- else the compiler waits at every join, i.e. every step,
+ * for all memory operations in flight (the symbol stores among them). */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HH_LOADS_DONE() __builtin_amdgcn_s_waitcnt(0)
+#else
+#define HH_LOADS_DONE() do {} while (0)
+#endif
+
 HH_HD uint32_t hh_tail_symbol(const hh_ctx *c, uint32_t p) {
     uint32_t node = 0;
     while (p < c->bt) {
@@ -166,7 +176,9 @@ HH_HD uint32_t hh_tail_symbol(const hh_ctx *c, uint32_t p) {
         node = hh_bit(c, p) ? (t >> 15) & 0x7fffu : t & 0x7fffu;
         p++;
     }
-    return c->tsym[node];
+    const uint32_t s = c->tsym[node];
+    HH_LOADS_DONE();
+    return s;
 }
 
 /* First code longer than HH_P bits: second-level table, then (very long
@@ -182,8 +194,8 @@ HH_HD uint32_t hh_escape(const hh_ctx *c, uint32_t p, uint32_t win, uint32_t m, 
     uint32_t node = e2 & 0xffffffu, d = HH_P + q;
     for (;;) {
         uint32_t t = c->tree[node];
-        if (t & HH_T_LEAF) { *sym = t & 0xffu; return d; }
-        if (p + d >= c->bt) { *sym = c->tsym[node]; return d; }
+        if (t & HH_T_LEAF) { *sym = t & 0xffu; HH_LOADS_DONE(); return d; }
+        if (p + d >= c->bt) { *sym = c->tsym[node]; HH_LOADS_DONE(); return d; }
         node = hh_bit(c, p + d) ? (t >> 15) & 0x7fffu : t & 0x7fffu;
         d++;
     }

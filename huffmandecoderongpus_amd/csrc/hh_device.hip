@@ -250,14 +250,15 @@ __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, 
 #define HH_EMIT_MINW 4
 #endif
 
-// Diagnostic build only (-DHH_DIAG): wave 0 of every workgroup stamps the
-// shader clock between the front kernel's phases and adds the cycles into
-// dbg[phase]; walk statistics go to dbg[8..]: lanes, lookups, the sum over
+// Diagnostic build only (-DHH_DIAG): every wave stamps the shader clock
+// between the front kernel's phases and adds the cycles into dbg[phase]
+// (0 staging, 4 own pass 1, 1 its barrier wait, 5 own walks, 2 their barrier
+// wait, 3 table); walk statistics go to dbg[8..]: lanes, lookups, the sum over
 // tiles of the longest walk, the longest walk.  hh_debug_counters reads them.
 #ifdef HH_DIAG
 #define DIAG_DECL uint64_t dg_acc[6] = {0, 0, 0, 0, 0, 0}, dg_w[4] = {0, 0, 0, 0}; uint64_t dg_t = __builtin_amdgcn_s_memtime();
 #define DIAG_STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); dg_acc[i] += t_ - dg_t; dg_t = t_; } while (0)
-#define DIAG_FLUSH(dbg) do { if (threadIdx.x == 0) for (int i_ = 0; i_ < 6; i_++) atomicAdd((unsigned long long *)&(dbg)[i_], (unsigned long long)dg_acc[i_]); \
+#define DIAG_FLUSH(dbg) do { if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 6; i_++) atomicAdd((unsigned long long *)&(dbg)[i_], (unsigned long long)dg_acc[i_]); \
     if ((threadIdx.x & 63u) == 0) { for (int i_ = 0; i_ < 3; i_++) atomicAdd((unsigned long long *)&(dbg)[8 + i_], (unsigned long long)dg_w[i_]); \
         atomicMax((unsigned long long *)&(dbg)[11], (unsigned long long)dg_w[3]); } } while (0)
 #else
@@ -334,6 +335,7 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
         }
         s_x[j] = x;
         s_n[j] = (uint16_t)n;
+        DIAG_STAMP(4);                                  // (own pass 1; then the barrier wait)
         __syncthreads();
         DIAG_STAMP(1);
         // region j+1's chain met this one in the overlap window: merged at
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
             dg_w[2] += mx;                               // per wave
             dg_w[3] = dg_w[3] > mx ? dg_w[3] : mx;
         }
+        DIAG_STAMP(5);                                  // (own walks; then the barrier wait)
         __syncthreads();
         DIAG_STAMP(2);
 #endif
@@ -868,8 +871,8 @@ struct hh_decoder {
     size_t grid_l2;            // and the L2 table size
     uint32_t grid_tree;        // and the LDS tree size
     // host staging of the evaluate() scope (hh_decode_host)
-    uint8_t *h_stage;
-    size_t h_stage_size;
+    uint8_t *h_stage;          // 2 x HH_HOST_CHUNK pinned (hh_decode_host)
+    hipEvent_t h_ev[2];
     void *d_in, *d_out;
     size_t d_in_size, d_out_size;
 };
@@ -933,7 +936,11 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
     if (d->d_dbg) hipFree(d->d_dbg);
     if (d->d_in) hipFree(d->d_in);
     if (d->d_out) hipFree(d->d_out);
-    if (d->h_stage) hipHostFree(d->h_stage);
+    if (d->h_stage) {
+        hipHostFree(d->h_stage);
+        hipEventDestroy(d->h_ev[0]);
+        hipEventDestroy(d->h_ev[1]);
+    }
     if (d->h_flags) hipHostFree(d->h_flags);
     for (int i = 0; i < 4; i++)
         if (d->ev[i]) hipEventDestroy(d->ev[i]);
@@ -1267,10 +1274,40 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
     return rc;
 }
 
-// evaluate() scope (decodeUtil.c:41-43 times the whole decoder call): the
-// payload is staged through a pinned buffer the decoder keeps, copied to a
-// device buffer it keeps, decoded, and the symbols copied back through the
-// same pinned buffer.  No allocation after the first call of a size.
+// evaluate() scope (decodeUtil.c:41-43 times the whole decoder call): host
+// payload in, host symbols out.  Copies go through two pinned chunk buffers
+// the decoder keeps (HH_HOST_CHUNK each): the CPU copy of one chunk into (or
+// out of) pinned memory overlaps the DMA of the other, both ways.  Device
+// buffers are kept too: no allocation after the first call of a size.
+#define HH_HOST_CHUNK ((size_t)64 << 20)
+static int host_pipe(hh_decoder *d, uint8_t *host, uint8_t *dev, size_t n, bool h2d) {
+    if (!n) return HH_OK;
+    const size_t nch = (n + HH_HOST_CHUNK - 1) / HH_HOST_CHUNK;
+    for (size_t i = 0; i < nch + 1; i++) {
+        // DMA chunk i (h2d: after the CPU has staged it; d2h: into its buffer)
+        if (i < nch) {
+            const size_t off = i * HH_HOST_CHUNK, len = n - off < HH_HOST_CHUNK ? n - off : HH_HOST_CHUNK;
+            uint8_t *pin = d->h_stage + (i & 1) * HH_HOST_CHUNK;
+            if (i >= 2) HIP_OK(hipEventSynchronize(d->h_ev[i & 1]));   // buffer free again
+            if (h2d) {
+                memcpy(pin, host + off, len);
+                HIP_OK(hipMemcpyAsync(dev + off, pin, len, hipMemcpyHostToDevice, d->stream));
+            } else {
+                HIP_OK(hipMemcpyAsync(pin, dev + off, len, hipMemcpyDeviceToHost, d->stream));
+            }
+            HIP_OK(hipEventRecord(d->h_ev[i & 1], d->stream));
+        }
+        // d2h: the CPU drains chunk i-1 while chunk i is in flight
+        if (!h2d && i >= 1) {
+            const size_t k = i - 1, off = k * HH_HOST_CHUNK;
+            const size_t len = n - off < HH_HOST_CHUNK ? n - off : HH_HOST_CHUNK;
+            HIP_OK(hipEventSynchronize(d->h_ev[k & 1]));
+            memcpy(host + off, d->h_stage + (k & 1) * HH_HOST_CHUNK, len);
+        }
+    }
+    return HH_OK;
+}
+
 extern "C" int hh_decode_host(hh_decoder *d, const uint8_t *data, uint64_t bits, uint8_t *out,
                               uint64_t cap, uint64_t *out_len) {
     if (!d || !out_len || (!data && bits) || (!out && cap)) return HH_ERR_ARG;
@@ -1281,23 +1318,20 @@ extern "C" int hh_decode_host(hh_decoder *d, const uint8_t *data, uint64_t bits,
     int rc = ensure_dev(&d->d_in, &d->d_in_size, nb + HH_PAYLOAD_PAD);
     if (!rc) rc = ensure_dev(&d->d_out, &d->d_out_size, ocap);
     if (rc) return rc;
-    const size_t stage = nb + HH_PAYLOAD_PAD > ocap ? nb + HH_PAYLOAD_PAD : ocap;
-    if (d->h_stage_size < stage) {
-        if (d->h_stage) HIP_OK(hipHostFree(d->h_stage));
-        d->h_stage = nullptr;
-        d->h_stage_size = 0;
-        if (hipHostMalloc((void **)&d->h_stage, stage, hipHostMallocDefault) != hipSuccess) return HH_ERR_NOMEM;
-        d->h_stage_size = stage;
+    if (!d->h_stage) {
+        if (hipHostMalloc((void **)&d->h_stage, 2 * HH_HOST_CHUNK, hipHostMallocDefault) != hipSuccess) {
+            d->h_stage = nullptr;
+            return HH_ERR_NOMEM;
+        }
+        if (hipEventCreateWithFlags(&d->h_ev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&d->h_ev[1], hipEventDisableTiming) != hipSuccess)
+            return HH_ERR_DEVICE;
     }
-    memcpy(d->h_stage, data, nb);
-    memset(d->h_stage + nb, 0, HH_PAYLOAD_PAD);
-    HIP_OK(hipMemcpyAsync(d->d_in, d->h_stage, nb + HH_PAYLOAD_PAD, hipMemcpyHostToDevice, d->stream));
-    rc = hh_decode_device(d, d->d_in, bits, d->d_out, cap, out_len, d->stream);
-    if (!rc && *out_len) {
-        HIP_OK(hipMemcpyAsync(d->h_stage, d->d_out, *out_len, hipMemcpyDeviceToHost, d->stream));
-        HIP_OK(hipStreamSynchronize(d->stream));
-        memcpy(out, d->h_stage, *out_len);
-    }
+    HIP_OK(hipMemsetAsync((uint8_t *)d->d_in + nb, 0, HH_PAYLOAD_PAD, d->stream));
+    rc = host_pipe(d, (uint8_t *)data, (uint8_t *)d->d_in, nb, true);
+    if (!rc) rc = hh_decode_device(d, d->d_in, bits, d->d_out, cap, out_len, d->stream);
+    if (!rc) rc = host_pipe(d, out, (uint8_t *)d->d_out, *out_len, false);
+    if (!rc) HIP_OK(hipStreamSynchronize(d->stream));
     return rc;
 }
 

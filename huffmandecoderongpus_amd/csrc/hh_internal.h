@@ -41,7 +41,9 @@
 
 #include <stdint.h>
 
+#ifndef HH_P
 #define HH_P 11                 /* L1 index bits                      */
+#endif
 #define HH_L1_SIZE (1u << HH_P)
 #define HH_Q_MAX 9              /* max L2 subtable index bits         */
 #define HH_L2_MAX 4096          /* L2 entries kept (LDS budget 16 KB) */

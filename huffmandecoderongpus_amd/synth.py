@@ -148,3 +148,157 @@ def verify_tiled(out, syn: Synthetic) -> bool:
                                       syn.text.unsqueeze(0).expand(syn.copies, L)):
         return False
     return bool(torch.equal(out[n:n + syn.tail_syms], syn.text[:syn.tail_syms]))
+
+
+# ---------------------------------------------------------------------------
+# i.i.d. variant: symbols drawn independently from kjv.txt's
+# unigram distribution, splitmix64 with seed 0x5EED5EED.  Symbol i uses the
+# generator output after i+1 increments (counter form, so every symbol is
+# drawn in parallel): z = mix(seed + (i+1) * 0x9E3779B97F4A7C15), r = z >> 32,
+# x = (r * T) >> 32 with T the text length, symbol = the byte b whose
+# cumulative count range [cum[b-1], cum[b]) holds x.  Encoded on the GPU with
+# the kjv.txt.huff codebook (codes LSB-first, the stream's bit order).
+# ---------------------------------------------------------------------------
+IID_SEED = 0x5EED5EED
+_GOLDEN = 0x9E3779B97F4A7C15
+_M1 = 0xBF58476D1CE4E5B9
+_M2 = 0x94D049BB133111EB
+
+
+def _s64(v: int) -> int:
+    """uint64 constant as the int64 torch arithmetic wraps in."""
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def _srl(z, k: int):
+    """Logical right shift of int64 tensors holding uint64 bit patterns."""
+    return (z >> k) & ((1 << (64 - k)) - 1)
+
+
+def splitmix64(idx, seed: int = IID_SEED):
+    """splitmix64 outputs for counters idx (int64 tensor, 0-based) as int64
+    bit patterns (torch) -- the numpy twin is splitmix64_np."""
+    z = idx.add(1).mul(_s64(_GOLDEN)).add(_s64(seed))
+    z = (z ^ _srl(z, 30)).mul(_s64(_M1))
+    z = (z ^ _srl(z, 27)).mul(_s64(_M2))
+    return z ^ _srl(z, 31)
+
+
+def splitmix64_np(idx: np.ndarray, seed: int = IID_SEED) -> np.ndarray:
+    """Host twin of splitmix64 (uint64 arithmetic wraps)."""
+    with np.errstate(over="ignore"):
+        z = (idx.astype(np.uint64) + np.uint64(1)) * np.uint64(_GOLDEN) + np.uint64(seed)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(_M1)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(_M2)
+        return z ^ (z >> np.uint64(31))
+
+
+def unigram_cum(text: np.ndarray) -> np.ndarray:
+    """Cumulative byte counts of the source text (int64[256])."""
+    return np.cumsum(np.bincount(text, minlength=256)).astype(np.int64)
+
+
+def iid_symbols_np(cum: np.ndarray, start: int, n: int, seed: int = IID_SEED) -> np.ndarray:
+    """Symbols start .. start+n-1 of the i.i.d. stream, on the host."""
+    T = int(cum[-1])
+    r = splitmix64_np(np.arange(start, start + n, dtype=np.uint64), seed) >> np.uint64(32)
+    x = ((r * np.uint64(T)) >> np.uint64(32)).astype(np.int64)
+    return np.searchsorted(cum, x, side="right").astype(np.uint8)
+
+
+def code_table(tree) -> tuple[np.ndarray, np.ndarray]:
+    """(code bits LSB-first = first branch in bit 0, code length) per byte."""
+    code = np.zeros(256, np.int64)
+    L = np.zeros(256, np.int64)
+    stack = [(0, 0, 0)]
+    while stack:
+        v, d, c = stack.pop()
+        if tree.izero[v] == -1:
+            s = tree.sym[v]
+            if L[s] == 0:
+                L[s], code[s] = d, c
+        else:
+            stack.append((int(tree.izero[v]), d + 1, c))
+            stack.append((int(tree.ione[v]), d + 1, c | (1 << d)))
+    if L.max() > 32:
+        raise ValueError("codes longer than 32 bits")
+    return code, L
+
+
+@dataclass
+class IIDStream:
+    tree: object            # huffmandecoderongpus_amd.Tree
+    data: object            # torch uint8 cuda tensor: payload + pad
+    bits: int
+    syms: object            # torch uint8 cuda tensor: the symbols encoded
+
+    @property
+    def compressed_bytes(self) -> int:
+        return (self.bits + 7) // 8
+
+    @property
+    def decoded_bytes(self) -> int:
+        return int(self.syms.numel())
+
+
+def encode_gpu(syms, code, lens, device="cuda", chunk: int = 1 << 27):
+    """Pack symbols (torch uint8) LSB-first with (code, lens) on the GPU ->
+    (payload uint8 tensor with 72 pad bytes, bits).  Codes of distinct
+    symbols occupy disjoint bits, so OR is a sum: 32-bit words are built by
+    index_add_ of each code's low and high parts in int64."""
+    import torch
+    codes = torch.as_tensor(code, device=device)
+    lt = torch.as_tensor(lens, device=device)
+    n = syms.numel()
+    total = 0
+    offs = []                                   # per-chunk start bits
+    for c0 in range(0, n, chunk):
+        offs.append(total)
+        total += int(lt[syms[c0:c0 + chunk].long()].sum().item())
+    nwords = (total + 31) // 32 + 2 + 18        # + pad (72 B)
+    words = torch.zeros(nwords, dtype=torch.int64, device=device)
+    for i, c0 in enumerate(range(0, n, chunk)):
+        s = syms[c0:c0 + chunk].long()
+        ln = lt[s]
+        pos = torch.cumsum(ln, 0) - ln + offs[i]
+        cv = codes[s]
+        w, sh = pos >> 5, pos & 31
+        words.index_add_(0, w, (cv << sh) & 0xffffffff)
+        words.index_add_(0, w + 1, cv >> (32 - sh))
+        del s, ln, pos, cv, w, sh
+    payload = words.to(torch.int32).view(torch.uint8)
+    return payload, total
+
+
+def iid_stream(hf, text: np.ndarray, target_bytes: int, device="cuda", seed: int = IID_SEED,
+               chunk: int = 1 << 27) -> IIDStream:
+    """The i.i.d. stream cut at the last whole symbol within target_bytes of
+    payload, encoded on the GPU with hf's codebook."""
+    import torch
+    tree = hf.tree()
+    code, lens = code_table(tree)
+    cum = unigram_cum(text)
+    T = int(cum[-1])
+    cum_t = torch.as_tensor(cum, device=device)
+    p = np.bincount(text, minlength=256) / T
+    n = int(8 * target_bytes / float((p * lens).sum()) * 1.01) + 64    # a little more than fits
+    syms = torch.empty(n, dtype=torch.uint8, device=device)
+    for c0 in range(0, n, chunk):
+        c1 = min(c0 + chunk, n)
+        r = _srl(splitmix64(torch.arange(c0, c1, dtype=torch.int64, device=device), seed), 32)
+        x = (r * T) >> 32
+        syms[c0:c1] = torch.searchsorted(cum_t, x, right=True).to(torch.uint8)
+        del r, x
+    lt = torch.as_tensor(lens, device=device)
+    # keep the longest prefix whose bits fit the target
+    budget, keep = 8 * target_bytes, 0
+    for c0 in range(0, n, chunk):
+        cs = torch.cumsum(lt[syms[c0:c0 + chunk].long()], 0)
+        k = int(torch.searchsorted(cs, torch.tensor([budget], device=device), right=True).item())
+        keep += k
+        if k < cs.numel():
+            break
+        budget -= int(cs[-1].item())
+    syms = syms[:keep].clone()
+    payload, bits = encode_gpu(syms, code, lens, device, chunk)
+    return IIDStream(tree, payload, bits, syms)

@@ -176,8 +176,8 @@ def test_capacity_error(hh, files_dir):
         dec.close()
 
 
-@pytest.mark.parametrize("mib", [64, 1024])
-def test_synthetic_full_size(hh, files_dir, mib):
+@pytest.mark.parametrize("src,mib", [("kjv.txt", 64), ("kjv.txt", 1024), ("E.coli", 1024)])
+def test_synthetic_full_size(hh, files_dir, src, mib):
     """BASELINE.json's workload size (1 GiB compressed): kjv.txt tiled and
     encoded with its own codebook must decode to the tiled text (a
     size-independent property; the text itself is sha256-pinned).  At this
@@ -185,11 +185,12 @@ def test_synthetic_full_size(hh, files_dir, mib):
     entered with d > 0 occur."""
     import torch
     from huffmandecoderongpus_amd import synth
-    hf, text = synth.load_source(files_dir)
+    hf, text = synth.load_source(files_dir, src)
     syn = synth.tiled_stream(hf, text, mib << 20)
     dec = hh.Decoder(0)
     try:
         dec.set_tree(syn.tree)
+        # (E.coli at 1 GiB: 4 GiB of output, past 2^31 and 2^32 output bytes)
         out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device="cuda")
         for _ in range(2):
             out.fill_(0xAB)
@@ -198,9 +199,76 @@ def test_synthetic_full_size(hh, files_dir, mib):
             assert n == syn.decoded_bytes
             assert synth.verify_tiled(out, syn)
             assert int(out[n:n + 64].ne(0xAB).sum()) == 0      # nothing written past the end
+            assert dec.stats()["exact_fallback"] == 0
     finally:
         dec.close()
         del out
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("mib", [64, 1024])
+def test_iid_stream(hh, files_dir, mib):
+    """SURVEY 8d's i.i.d. variant: kjv unigram symbols from splitmix64 (seed
+    0x5EED5EED), encoded on the GPU; the decode must return the symbols.  At
+    64 MiB the first 1 M symbols are also checked against the host generator
+    and the GPU payload's first 256 KiB against the host encoder."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    hf, text = synth.load_source(files_dir)
+    s = synth.iid_stream(hf, text, mib << 20)
+    if mib == 64:
+        n0 = 1 << 20
+        assert np.array_equal(s.syms[:n0].cpu().numpy(),
+                              synth.iid_symbols_np(synth.unigram_cum(text), 0, n0))
+        pay, bits = hf.tree().encode(s.syms[:n0].cpu().numpy())
+        assert np.array_equal(s.data[: 1 << 18].cpu().numpy(), pay[: 1 << 18])
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(s.tree)
+        out = torch.full((s.decoded_bytes + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+        n = dec.decode_device(s.data, s.bits, out)
+        torch.cuda.synchronize()
+        assert n == s.decoded_bytes
+        assert torch.equal(out[:n], s.syms)
+        assert int(out[n:n + 64].ne(0xAB).sum()) == 0
+        assert dec.stats()["exact_fallback"] == 0
+    finally:
+        dec.close()
+        del out, s
+        torch.cuda.empty_cache()
+
+
+def test_hufx_over_2gib_save_reload_decode(hh, files_dir, tmp_path):
+    """The 64-bit container end to end: a 2.25 GiB kjv-tiled payload (more
+    than 2^34 bits, beyond the reference's int32 header) written with
+    hh_huff_save, loaded back with hh_huff_load and decoded on the GPU."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    hf, text = synth.load_source(files_dir)
+    syn = synth.tiled_stream(hf, text, (9 << 30) // 4)
+    assert syn.bits > 1 << 34
+    nb = syn.compressed_bytes
+    data = np.zeros(nb + hh.PAYLOAD_PAD, np.uint8)
+    data[:nb] = syn.data[:nb].cpu().numpy()
+    big = hh.HuffFile(syn.tree.izero, syn.tree.ione, syn.tree.sym, syn.bits, syn.decoded_bytes, data)
+    path = str(tmp_path / "kjv_2g.huff")
+    big.save(path)
+    del big
+    back = hh.HuffFile.load(path)
+    assert back.bits == syn.bits and back.uncompressedsize == syn.decoded_bytes
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(back.tree())
+        d_in = torch.from_numpy(back.data).cuda()
+        del back
+        out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device="cuda")
+        n = dec.decode_device(d_in, syn.bits, out)
+        torch.cuda.synchronize()
+        assert n == syn.decoded_bytes
+        assert synth.verify_tiled(out, syn)
+    finally:
+        dec.close()
+        os.remove(path)
         torch.cuda.empty_cache()
 
 

@@ -57,9 +57,15 @@ if os.environ.get("HH_DIAG"):            # a -DHH_DIAG build: phase cycles and w
     import ctypes as C
     buf = (C.c_uint64 * 16)()
     H.lib().hh_debug_counters(dec._h, buf)
-    cyc = [buf[i] for i in range(4)]
+    cyc = [buf[i] for i in range(6)]
     tot = sum(cyc) or 1
-    res["front_phase_frac"] = {n: round(v / tot, 3) for n, v in zip(("stage", "pass1", "walks", "table"), cyc)}
+    res["front_phase_frac"] = {n: round(cyc[i] / tot, 3) for n, i in
+                               (("stage", 0), ("pass1", 4), ("pass1_wait", 1), ("walks", 5),
+                                ("walks_wait", 2), ("table", 3))}
+    ecyc = [buf[i] for i in (6, 7, 12, 13, 14)]
+    etot = sum(ecyc) or 1
+    res["emit_phase_frac"] = {n: round(v / etot, 3) for n, v in
+                              zip(("records_scan", "zero", "decode", "decode_wait", "copyout"), ecyc)}
     if buf[8]:
         res["walk"] = {"mean_steps": round(buf[9] / buf[8], 2), "mean_wave_max": round(buf[10] / (buf[8] / 64), 2),
                        "max": buf[11]}
