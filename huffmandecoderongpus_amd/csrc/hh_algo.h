@@ -50,25 +50,25 @@
 
 /* ------------------------------------------------------------------ */
 /* Tile geometry.                                                       */
-/*   HH_NL lanes per tile (one workgroup), lane j owns region j of S     */
-/*   bits.  A walk may cross up to HH_KM regions before it merges (runs */
-/*   of a repeated symbol keep chains apart for hundreds of bits), so   */
-/*   the tile stages HH_KM regions of the next tile too, plus a halo     */
-/*   for codes running past the last one.                                */
+/*   A tile is HH_NR = 64 regions of S bits, one WAVE: lane j owns       */
+/*   region j, and everything up to the tile's transfer table happens    */
+/*   inside the wave (no workgroup barrier, so a wave with a long walk   */
+/*   holds up only itself).  A walk may cross up to HH_KM regions before */
+/*   it merges (runs of a repeated symbol keep chains apart for hundreds */
+/*   of bits), so a tile stages HH_KM regions of the next tile too, plus */
+/*   a halo for codes running past the last one.                         */
 /*   The bitstream is staged in LDS TRANSPOSED: tile word g lives at     */
-/*   (g % sw) * HH_NLS + g / sw, i.e. region r is column r.  Lanes read  */
-/*   their own columns, so a wave's reads fall in distinct banks         */
-/*   (HH_NLS is a multiple of 32) however far apart the lanes' chains    */
-/*   are.                                                                */
+/*   (g % sw) * nls + g / sw, i.e. region r is column r.  Lanes read     */
+/*   their own columns, so a wave's reads fall in distinct banks (nls is */
+/*   a multiple of 32) however far apart the lanes' chains are.  The     */
+/*   emission kernel stages groups of several tiles with its own stride  */
+/*   (hh_ctx.nls).                                                       */
 /* ------------------------------------------------------------------ */
-#ifndef HH_NL
-#define HH_NL 256
-#endif
-#define HH_NR HH_NL           /* regions per tile */
+#define HH_NR 64              /* regions per tile (a wave) */
 #define HH_KM 8               /* max regions one walk may cross */
 #define HH_NCOL (HH_NR + HH_KM + 1)   /* staged columns */
 #ifndef HH_NLS
-#define HH_NLS 288            /* >= HH_NCOL, multiple of 32 */
+#define HH_NLS 96             /* column stride of a tile's staging: >= HH_NCOL, multiple of 32 */
 #endif
 #define HH_SW_MAX 12          /* max words per region (S <= 384) */
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
@@ -103,6 +103,7 @@ HH_HD uint32_t hh_magic(uint32_t sw) { return (uint32_t)((0x100000000ull + sw - 
 typedef struct {
     const uint32_t *w;    /* transposed tile words                        */
     uint32_t sw;          /* words per region                             */
+    uint32_t nls;         /* column stride of the staged words            */
     uint32_t magic;       /* hh_magic(sw)                                 */
     const uint32_t *l1m;  /* HH_L1_SIZE entries: the meta half (bits 32..63
                              of the hh_internal.h L1 entry; HH_M_*)      */
@@ -122,12 +123,12 @@ typedef struct {
  * a compile-time sw), so this division folds to shifts / a multiply-high. */
 HH_HD uint32_t hh_idx(const hh_ctx *c, uint32_t g) {
     const uint32_t r = g / c->sw;
-    return (g - r * c->sw) * HH_NLS + r;
+    return (g - r * c->sw) * c->nls + r;
 }
 /* LDS index of the word after the one at index a */
 HH_HD uint32_t hh_idx_next(const hh_ctx *c, uint32_t a) {
-    const uint32_t last = (c->sw - 1) * HH_NLS;
-    return a >= last ? a - last + 1 : a + HH_NLS;
+    const uint32_t last = (c->sw - 1) * c->nls;
+    return a >= last ? a - last + 1 : a + c->nls;
 }
 HH_HD uint32_t hh_word(const hh_ctx *c, uint32_t g) { return c->w[hh_idx(c, g)]; }
 
@@ -339,16 +340,27 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
  * [s, R) as bits of *head (bit i <=> a symbol starts at s + i).  Pass 1 then
  * counts C_r from y, exactly as a chain started at y (so counts, masks and
  * walks keep the offset-0 semantics with R's entry point y instead of R). */
-HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, uint64_t *head) {
-    uint64_t h = 0;
+#define HH_GMAX 128u          /* largest overlap */
+typedef struct {
+    uint64_t lo, hi;          /* boundary bits of [s, s + 128) */
+} hh_head;
+
+HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, hh_head *head) {
+    uint64_t lo = 0, hi = 0;
     hh_cur u = hh_cur_at(c, s);
     while (u.p < R && u.p < c->bt) {
         hh_look L = hh_lookup_w(c, u.p, hh_cur_win(u));
         const uint32_t o = hh_first_ge(L, R - u.p);     /* first start >= R, or nb */
-        h |= (uint64_t)(L.bm & hh_lowmask(o)) << (u.p - s);
+        const uint64_t v = L.bm & hh_lowmask(o);
+        const uint32_t off = u.p - s;                   /* < 128 */
+        lo |= off < 64 ? v << off : 0ull;
+        hi |= off >= 64 ? v << (off - 64) : off > 32 ? v >> (64 - off) : 0ull;
         hh_cur_adv(c, u, o);
     }
-    if (head) *head = h;
+    if (head) {
+        head->lo = lo;
+        head->hi = hi;
+    }
     return u.p < c->bt ? u.p : c->bt;
 }
 
@@ -357,11 +369,15 @@ HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, uint64_t 
  * bits there meet C_{j+1}'s head bits: then the chains are identical from
  * that boundary on, C_j's exit is C_{j+1}'s entry point y, and the walk
  * from C_j's exit merges at once (k = 1, delta = 0). */
-HH_HD bool hh_window_merge(const hh_ctx *c, const uint32_t *mask, uint64_t head_next, uint32_t R) {
-    uint64_t mine = 0;
-    for (uint32_t w = 0; w < c->G / 32; w++)
-        mine |= (uint64_t)mask[hh_idx(c, (R - c->G) / 32 + w + 2)] << (32 * w);
-    return (mine & head_next) != 0;
+HH_HD bool hh_window_merge(const hh_ctx *c, const uint32_t *mask, hh_head next, uint32_t R) {
+    uint64_t mlo = 0, mhi = 0;
+    const uint32_t g0 = (R - c->G) / 32 + 2;
+    for (uint32_t w = 0; w < c->G / 32; w++) {
+        const uint64_t v = mask[hh_idx(c, g0 + w)];
+        if (w < 2) mlo |= v << (32 * w);
+        else mhi |= v << (32 * (w - 2));
+    }
+    return ((mlo & next.lo) | (mhi & next.hi)) != 0;
 }
 
 /* Symbols of a region's own chain that start before region offset off
@@ -589,9 +605,12 @@ HH_HD uint64_t hh_inc_prefix(uint64_t g) { return (uint64_t)((int64_t)(g << 24) 
  * starts on the code-length lattice (a multiple of the length gcd); none
  * for a fixed-length code (its chains sit on one lattice and merge at
  * once). */
+#ifndef HH_OVERLAP_BITS
+#define HH_OVERLAP_BITS 64u
+#endif
 HH_HD uint32_t hh_pick_overlap(const hh_tables *t) {
     const uint32_t g = t->len_gcd > 0 ? (uint32_t)t->len_gcd : 1u;
-    return t->fixed_len > 0 || 64u % g ? 0u : 64u;
+    return t->fixed_len > 0 || HH_OVERLAP_BITS % g ? 0u : HH_OVERLAP_BITS;
 }
 
 /* Region size for a code whose lengths are all multiples of g: a multiple

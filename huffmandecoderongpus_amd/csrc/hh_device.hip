@@ -38,10 +38,16 @@
 #include "hiphuff.h"
 
 #define HH_MAXLEN_FAST 32           // longest code of the fast path (one cursor step <= 32 bits)
+#define HH_NL 256                   // lanes per workgroup (both kernels)
 #define HH_NW (HH_NL / 64)          // waves per workgroup
+// k_emit works on groups of HH_NW consecutive tiles, one per wave, staged
+// together (one output staging buffer and one scan per group)
+#define HH_GR (HH_NW * HH_NR)       // regions per group
+#define HH_GCOL (HH_GR + HH_KM + 1) // staged columns
+#define HH_GNLS 288                 // their column stride (>= HH_GCOL, multiple of 32)
 #define HH_SCAN_TB 1024             // tiles per k_scan1 block
 #define HH_SCAN_BACK 4096           // longest non-CONST chain k_scan1 composes (else host scan)
-#define HH_OB (16384 + 64)          // k_emit's LDS output staging (bytes): a text tile's output
+#define HH_OB (16384 + 64)          // k_emit's LDS output staging (bytes): a text group's output
                                     // (<= ~15.2 K symbols for kjv) plus the 16-B phase
 
 #define HIP_OK(x)                                                             \
@@ -101,7 +107,7 @@ struct Geometry {
 struct Work {
     uint32_t *flags;     // 64 B
     uint64_t *tabs;      // [ntiles][HH_KM] rows: count | state << 20; row 0 bit 61 = CONST
-    uint32_t *recs;      // [ntiles][HH_NR] lane records
+    uint32_t *recs;      // [ntiles][HH_NR] lane records (a group's are contiguous)
     uint32_t *st;        // [ntiles + 1] state entering each tile (st[ntiles]: leaving the last)
     int32_t *lex;        // [ntiles + 1] exclusive prefix of charged counts within its scan block
     int64_t *blk;        // [nblk] scan block totals, then exclusive block bases
@@ -146,90 +152,118 @@ __device__ __forceinline__ int32_t block_excl_scan(int32_t v, int32_t *s_tmp, in
     return base + x - v;
 }
 
-// Stream word gi, zero past the readable payload.
-__device__ __forceinline__ uint32_t ld_word(const uint32_t *g, uint64_t gi, uint64_t nok) {
-    return gi < nok ? __builtin_nontemporal_load(&g[gi]) : 0u;
+// Words of a staged span through a buffer resource over its readable words:
+// the range check returns 0 past the payload, so no lane branches between
+// load paths (with a per-lane branch the compiler waits for every load in
+// flight before the second path's loads).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t words_rsrc(const uint32_t *g, uint64_t tw0, uint64_t nok) {
+    const uint64_t left = nok > tw0 ? nok - tw0 : 0u;
+    const uint32_t nbytes = left > 0x3fffffffull ? 0xfffffffcu : (uint32_t)left * 4u;
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(g + tw0), 0, (int)nbytes, 0x00020000);
 }
 
-// Registers holding one tile's words for this lane: its region column and,
-// for lanes < (HH_NCOL - HH_NR) * sw, one word of the columns past the tile
-// (the next tile's first HH_KM regions and the halo).
-#define HH_XW ((HH_NCOL - HH_NR) * HH_SW_MAX)
-static_assert(HH_XW <= HH_NL, "extra columns must fit one word per lane");
-static_assert(HH_NLS >= HH_NCOL && HH_NLS % 32 == 0, "LDS column stride");
-struct Prefetch {
-    uint32_t v[HH_SW_MAX];
-    uint32_t halo;
-};
-
 template <uint32_t sw>
-__device__ __forceinline__ void prefetch_tile(Prefetch &pf, const uint32_t *g, uint64_t tw0,
-                                              uint64_t nok, bool vec4) {
-    const uint32_t j = threadIdx.x;
-    const uint64_t gi = tw0 + (uint64_t)j * sw;
-    if (sw % 4 == 0 && vec4 && gi + HH_SW_MAX <= nok) {
+__device__ __forceinline__ void load_region(uint32_t *v, __amdgpu_buffer_rsrc_t r, uint32_t col) {
+    const uint32_t v0 = 4u * col * sw;
+    if (sw % 4 == 0) {
 #pragma unroll
         for (uint32_t k = 0; k < HH_SW_MAX; k += 4) {
             if (k < sw) {
-                const u32x4 q = __builtin_nontemporal_load((const u32x4 *)(g + gi + k));
-                pf.v[k] = q.x; pf.v[k + 1] = q.y; pf.v[k + 2] = q.z; pf.v[k + 3] = q.w;
+                const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(v0 + 4u * k), 0, 0));
+                v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
             }
         }
     } else {
 #pragma unroll
         for (uint32_t k = 0; k < HH_SW_MAX; k++)
-            if (k < sw) pf.v[k] = ld_word(g, gi + k, nok);
+            if (k < sw) v[k] = __builtin_amdgcn_raw_buffer_load_b32(r, (int)(v0 + 4u * k), 0, 0);
     }
-    pf.halo = j < (HH_NCOL - HH_NR) * sw ? ld_word(g, tw0 + (uint64_t)HH_NR * sw + j, nok) : 0u;
 }
 
+// Registers holding one tile's (k_front) or group's (k_emit) words for this
+// lane: its region column and up to two words of the columns past the span
+// (the next tile's first HH_KM regions and the halo).
+static_assert((HH_NCOL - HH_NR) * HH_SW_MAX <= 2 * 64, "a tile's extra columns: two words per lane");
+static_assert((HH_GCOL - HH_GR) * HH_SW_MAX <= HH_NL, "a group's extra columns: one word per lane");
+static_assert(HH_NLS >= HH_NCOL && HH_NLS % 16 == 0 && HH_GNLS >= HH_GCOL && HH_GNLS % 32 == 0,
+              "LDS column strides");
+struct Prefetch {
+    uint32_t v[HH_SW_MAX];
+    uint32_t halo, halo2;
+};
+
+// k_front: a wave's tile (lane = its region)
 template <uint32_t sw>
-__device__ __forceinline__ void store_tile(const Prefetch &pf, uint32_t *s_w) {
-    const uint32_t j = threadIdx.x;
+__device__ __forceinline__ void prefetch_wtile(Prefetch &pf, const uint32_t *g, uint64_t tw0, uint64_t nok) {
+    const uint32_t j = threadIdx.x & 63u;
+    const __amdgpu_buffer_rsrc_t r = words_rsrc(g, tw0, nok);
+    load_region<sw>(pf.v, r, j);
+    constexpr uint32_t nx = (HH_NCOL - HH_NR) * sw;
+    pf.halo = j < nx ? __builtin_amdgcn_raw_buffer_load_b32(r, (int)(4u * (HH_NR * sw + j)), 0, 0) : 0u;
+    pf.halo2 = j + 64 < nx ? __builtin_amdgcn_raw_buffer_load_b32(r, (int)(4u * (HH_NR * sw + j + 64)), 0, 0) : 0u;
+}
+template <uint32_t sw>
+__device__ __forceinline__ void store_wtile(const Prefetch &pf, uint32_t *s_w) {
+    const uint32_t j = threadIdx.x & 63u;
+    constexpr uint32_t nx = (HH_NCOL - HH_NR) * sw;
 #pragma unroll
     for (uint32_t k = 0; k < HH_SW_MAX; k++)
         if (k < sw) s_w[k * HH_NLS + j] = pf.v[k];
-    if (j < (HH_NCOL - HH_NR) * sw) s_w[(j % sw) * HH_NLS + HH_NR + j / sw] = pf.halo;
+    if (j < nx) s_w[(j % sw) * HH_NLS + HH_NR + j / sw] = pf.halo;
+    if (j + 64 < nx) s_w[((j + 64) % sw) * HH_NLS + HH_NR + (j + 64) / sw] = pf.halo2;
 }
 
-// The walks with k > 1 (exceptions) of a tile, ascending, into s_exc.
-__device__ __forceinline__ uint32_t collect_exceptions(bool is_exc, uint16_t *s_exc, uint32_t *s_cnt) {
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const uint64_t m = __ballot(is_exc);
-    if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(m);
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < HH_NW; i++) {
-        off += i < wv ? s_cnt[i] : 0u;
-        tot += s_cnt[i];
-    }
-    if (is_exc) {
-        const uint64_t below = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
-        s_exc[off + (uint32_t)__popcll(below)] = (uint16_t)threadIdx.x;
-    }
-    __syncthreads();
-    return tot;
-}
-
-// Live masks over the entering state d (bit d of s_mem[j]: lane j is live
-// when the tile is entered in region d): hh_mem_init, then the exceptions in
-// ascending lane order clear the lanes their walks cover.  One lane; there
-// are rarely more than a couple of exceptions per tile.
-__device__ __forceinline__ void resolve_live(uint32_t kk, uint8_t *s_k, uint8_t *s_mem, uint16_t *s_exc,
-                                             uint32_t *s_cnt) {
+// k_emit: a workgroup's group of tiles (lane = its region within the group)
+template <uint32_t sw>
+__device__ __forceinline__ void prefetch_group(Prefetch &pf, const uint32_t *g, uint64_t tw0, uint64_t nok) {
     const uint32_t j = threadIdx.x;
+    const __amdgpu_buffer_rsrc_t r = words_rsrc(g, tw0, nok);
+    load_region<sw>(pf.v, r, j);
+    constexpr uint32_t nx = (HH_GCOL - HH_GR) * sw;
+    pf.halo = j < nx ? __builtin_amdgcn_raw_buffer_load_b32(r, (int)(4u * (HH_GR * sw + j)), 0, 0) : 0u;
+}
+template <uint32_t sw>
+__device__ __forceinline__ void store_group(const Prefetch &pf, uint32_t *s_w) {
+    const uint32_t j = threadIdx.x;
+#pragma unroll
+    for (uint32_t k = 0; k < HH_SW_MAX; k++)
+        if (k < sw) s_w[k * HH_GNLS + j] = pf.v[k];
+    if (j < (HH_GCOL - HH_GR) * sw) s_w[(j % sw) * HH_GNLS + HH_GR + j / sw] = pf.halo;
+}
+
+// Lanes of one wave exchanging values through LDS: a wave's LDS operations
+// execute in order, so a compiler fence is all the ordering needed.
+#define WAVE_SYNC()                                                    \
+    do {                                                               \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");         \
+        __builtin_amdgcn_wave_barrier();                               \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");         \
+    } while (0)
+
+// Live masks over the entering state d of a wave's tile (bit d of mem: the
+// lane is live when the tile is entered in region d): hh_mem_init, then the
+// walks with k > 1 (exceptions), in ascending lane order, clear the lanes
+// they cover (within the tile).  s_k, s_mem: the wave's 64 entries.  One
+// lane; a tile rarely has more than one exception.
+__device__ __forceinline__ uint32_t resolve_live_wave(uint32_t kk, uint8_t *s_k, uint8_t *s_mem) {
+    const uint32_t j = threadIdx.x & 63u;
+    const uint64_t ex = __ballot(kk > 1);
+    if (ex == 0) return hh_mem_init(j);
     s_k[j] = (uint8_t)kk;
     s_mem[j] = (uint8_t)hh_mem_init(j);
-    const uint32_t nexc = collect_exceptions(kk > 1, s_exc, s_cnt);   // barriers inside
+    WAVE_SYNC();
     if (j == 0) {
-        for (uint32_t i = 0; i < nexc; i++) {
-            const uint32_t e = s_exc[i], ke = s_k[e];
-            const uint8_t m = s_mem[e];
-            for (uint32_t q = e + 1; q < e + ke && q < HH_NR; q++) s_mem[q] &= (uint8_t)~m;
+        uint64_t m = ex;
+        while (m) {
+            const uint32_t e = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t ke = s_k[e];
+            const uint8_t me = s_mem[e];
+            for (uint32_t q = e + 1; q < e + ke && q < HH_NR; q++) s_mem[q] &= (uint8_t)~me;
         }
     }
-    __syncthreads();
+    WAVE_SYNC();
+    return s_mem[j];
 }
 
 // Decode tables into LDS (meta halves always; symbol halves when s_l1s).
@@ -268,36 +302,42 @@ __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, 
 #endif
 
 // ---------------------------------------------------------------------------
-// k_front: pass 1, walks and the transfer table of every tile
+// k_front: pass 1, walks and the transfer table of every tile, one tile per
+// wave at a time (a persistent grid; wave gw takes tiles gw, gw + #waves,
+// ...).  Within a tile the lanes exchange values through the wave's own LDS
+// slice, never with other waves: no workgroup barrier after the tables.
 // ---------------------------------------------------------------------------
 template <uint32_t SW>
 __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *__restrict__ gdata, Geometry geo,
                                                                  DevTab tab, Work wk, uint64_t *dbg) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ uint32_t s_x[HH_NR];            // pass-1 exits
-    __shared__ uint16_t s_n[HH_NR];            // pass-1 counts
-    __shared__ uint8_t s_k[HH_NR];
-    __shared__ uint8_t s_mem[HH_NR];
-    __shared__ uint16_t s_exc[HH_NR];
-    __shared__ uint32_t s_cnt[HH_NW];
-    __shared__ int32_t s_part[HH_NW];
-    __shared__ int32_t s_cd[HH_KM];            // per-d counts of the partially live lanes
-    __shared__ uint32_t s_ost[HH_KM];          // per-d leaving states
+    __shared__ uint32_t s_xa[HH_NW][HH_NR];    // pass-1 exits
+    __shared__ uint16_t s_na[HH_NW][HH_NR];    // pass-1 counts
+    __shared__ uint8_t s_ka[HH_NW][HH_NR];
+    __shared__ uint8_t s_mema[HH_NW][HH_NR];
+    __shared__ int32_t s_cda[HH_NW][HH_KM];    // per-d counts of the partially live lanes
+    __shared__ uint32_t s_osta[HH_NW][HH_KM];  // per-d leaving states
 
     constexpr uint32_t S = 32 * SW;
-    uint32_t *s_l1m = (uint32_t *)smem;                 // L1 meta halves
-    uint32_t *s_w = s_l1m + HH_L1_SIZE;                 // SW * HH_NLS words (transposed)
+    const uint32_t j = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    uint32_t *s_l1m = (uint32_t *)smem;                 // L1 meta halves (shared)
+    uint32_t *s_l2 = s_l1m + HH_L1_SIZE;                // L2 (shared), then the waves' slices:
+    uint32_t *s_w = s_l2 + ((tab.l2_used + 3u) & ~3u) + wv * (2 * SW * HH_NLS);   // SW * HH_NLS words
     uint32_t *s_mk = s_w + SW * HH_NLS;                 // SW * HH_NLS boundary-mask words
-    uint32_t *s_l2 = s_mk + SW * HH_NLS;
+    uint32_t *s_x = s_xa[wv];
+    uint16_t *s_n = s_na[wv];
+    int32_t *s_cd = s_cda[wv];
+    uint32_t *s_ost = s_osta[wv];
 
-    const uint32_t j = threadIdx.x;
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
     const uint32_t span = HH_NCOL * S;                  // bits staged per tile
     load_tables(tab, s_l1m, nullptr, s_l2);
+    __syncthreads();                                    // (the only workgroup barrier)
 
     hh_ctx c;
     c.w = s_w;
     c.sw = SW;
+    c.nls = HH_NLS;
     c.magic = 0;
     c.l1m = s_l1m;
     c.l1s = nullptr;
@@ -307,27 +347,34 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
     c.maxadv = geo.maxadv;
     c.G = geo.G;
 
+    // The next tile's words are loaded one tile ahead into registers and
+    // stored to LDS once the walks are done (before the tile's record
+    // stores: vmcnt retires in order and counts stores too).  The loads run
+    // unconditionally (the last tile again past the end): a conditional load
+    // merges two values, which the compiler waits for.
+    const uint64_t nwv = (uint64_t)gridDim.x * HH_NW;
+    const uint64_t tlast = geo.ntiles ? geo.ntiles - 1 : 0;
+    auto clampt = [&](uint64_t tt) { return tt < tlast ? tt : tlast; };
     Prefetch pf;
-    uint64_t t = blockIdx.x;
-    if (t < geo.ntiles) prefetch_tile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords, geo.vec4);
+    uint64_t t = (uint64_t)blockIdx.x * HH_NW + wv;
+    if (t < geo.ntiles) {
+        prefetch_wtile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords);
+        store_wtile<SW>(pf, s_w);
+        prefetch_wtile<SW>(pf, gdata, clampt(t + nwv) * tile_bits / 32, geo.nwords);
+    }
     DIAG_DECL
-    for (; t < geo.ntiles; t += gridDim.x) {
-        __syncthreads();                                // previous tile's LDS no longer read
+    for (; t < geo.ntiles; t += nwv) {
+        WAVE_SYNC();                                    // this tile's words stored
         const uint64_t rem = geo.bits - t * tile_bits;
         c.bt = rem < span ? (uint32_t)rem : span;
         const uint32_t bt = c.bt;
-        store_tile<SW>(pf, s_w);
-        const uint64_t tn = t + gridDim.x;
-        if (tn < geo.ntiles) prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
-        __syncthreads();
         DIAG_STAMP(0);
 
-        // pass 1: own region from offset 0
         // pass 1: the head (from G bits before the region, lanes > 0), then
         // the own chain from its entry point y, counted and masked
         const uint32_t p0 = j * S;
         uint32_t n = 0, x = bt;
-        uint64_t head = 0;
+        hh_head head = {0ull, 0ull};
         if (p0 < bt) {
             const uint32_t y = j > 0 && c.G ? hh_region_head(&c, p0 - c.G, p0, &head) : p0;
             const uint32_t lim = p0 + S < bt ? p0 + S : bt;
@@ -335,25 +382,25 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
         }
         s_x[j] = x;
         s_n[j] = (uint16_t)n;
-        DIAG_STAMP(4);                                  // (own pass 1; then the barrier wait)
-        __syncthreads();
+        WAVE_SYNC();
         DIAG_STAMP(1);
         // region j+1's chain met this one in the overlap window: merged at
-        // this chain's exit, no walk.  Its head comes from the next lane of
-        // the wave; the last lane of a wave walks (one lookup when merged).
+        // this chain's exit, no walk.  Its head comes from the next lane; the
+        // last lane walks into the next tile (two pointers).
         const uint32_t R1 = (j + 1) * S;
-        const uint32_t hlo = (uint32_t)__shfl_down((int)(uint32_t)head, 1, 64);
-        const uint32_t hhi = (uint32_t)__shfl_down((int)(uint32_t)(head >> 32), 1, 64);
-        const bool merged = c.G && (j & 63u) != 63u && R1 < bt &&
-                            hh_window_merge(&c, s_mk, ((uint64_t)hhi << 32) | hlo, R1);
+        auto shfl64 = [](uint64_t v) {
+            const uint32_t a = (uint32_t)__shfl_down((int)(uint32_t)v, 1, 64);
+            const uint32_t b = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1, 64);
+            return ((uint64_t)b << 32) | a;
+        };
+        hh_head nh;
+        nh.lo = shfl64(head.lo);
+        nh.hi = c.G > 64 ? shfl64(head.hi) : 0ull;
+        const bool merged = c.G && j != 63u && R1 < bt && hh_window_merge(&c, s_mk, nh, R1);
 
         // walks: region j's exit against the next regions' own chains
-#ifndef HH_EXP_NOWALK
         hh_wk w = {1u, x - R1, 0u, 0, 0u, 0u};
         if (!merged) w = hh_walk(&c, j, S, x, s_mk, s_x, s_n, HH_NR);
-#else
-        const hh_wk w = {1u, 0u, 0u, 0, 0u, 0u};
-#endif
         if (w.k == 0) {
             atomicOr(wk.flags, (uint32_t)F_FAIL);
             if (atomicCAS(&wk.flags[4], 0u, 1u) == 0u) {
@@ -372,43 +419,43 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
             }
             dg_w[0] += 64;
             dg_w[1] += sm;
-            dg_w[2] += mx;                               // per wave
+            dg_w[2] += mx;
             dg_w[3] = dg_w[3] > mx ? dg_w[3] : mx;
         }
-        DIAG_STAMP(5);                                  // (own walks; then the barrier wait)
-        __syncthreads();
-        DIAG_STAMP(2);
 #endif
+        DIAG_STAMP(2);
         const uint32_t kk = w.k ? w.k : 1u;
-        if (j < HH_KM) s_cd[j] = 0;
-        resolve_live(kk, s_k, s_mem, s_exc, s_cnt);     // barriers inside
+        const uint32_t mem = resolve_live_wave(kk, s_ka[wv], s_mema[wv]);
+        // the walks are done: the next tile's words go to LDS now, and the
+        // tile after it is loaded
+        WAVE_SYNC();
+        store_wtile<SW>(pf, s_w);
+        prefetch_wtile<SW>(pf, gdata, clampt(t + 2 * nwv) * tile_bits / 32, geo.nwords);
 
         // transfer table: charged count and leaving state for every entering d
-        const uint32_t mem = s_mem[j];
         const int32_t charged = (int32_t)(n + w.cov) + w.delta;
+        if (j < HH_KM) s_cd[j] = 0;
+        WAVE_SYNC();
         if (j + kk >= HH_NR) {
             const uint32_t os = hh_state_pack(j + kk - HH_NR, w.e, w.delta);
 #pragma unroll
             for (uint32_t d = 0; d < HH_KM; d++)
                 if ((mem >> d) & 1u) s_ost[d] = os;
         }
-        // lanes live for every entering d: one block sum; the few others
+        // lanes live for every entering d: one wave sum; the few others
         // (lanes < HH_KM, covered lanes): per-d LDS atomics
         const uint32_t full = (1u << HH_KM) - 1u;
         const int32_t v = wave_sum(mem == full ? charged : 0);
-        if ((j & 63u) == 0) s_part[j >> 6] = v;
         if (mem != full) {
 #pragma unroll
             for (uint32_t d = 0; d < HH_KM; d++)
                 if ((mem >> d) & 1u) atomicAdd(&s_cd[d], charged);
         }
+        WAVE_SYNC();
         wk.recs[t * HH_NR + j] = rec_pack(kk, w.e, w.delta, n + w.cov);
-        __syncthreads();
-        if (j < 64) {
+        {
             const uint32_t dd = j < HH_KM ? j : 0u;
-            int32_t cnt = s_cd[dd];
-#pragma unroll
-            for (uint32_t i = 0; i < HH_NW; i++) cnt += s_part[i];
+            const int32_t cnt = s_cd[dd] + v;
             const uint32_t os = s_ost[dd];
             // CONST: the leaving state is the same for every entering d
             const bool cst = __ballot(j < HH_KM && os != s_ost[0]) == 0;
@@ -430,6 +477,7 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
 // tiles' charged counts -> lex, block total -> blk.
 __global__ __launch_bounds__(HH_SCAN_TB) void k_scan1(Geometry geo, Work wk) {
     __shared__ int32_t s_tmp[HH_SCAN_TB / 64];
+    __shared__ uint32_t s_cf;
     const uint64_t t = (uint64_t)blockIdx.x * HH_SCAN_TB + threadIdx.x;
     const bool valid = t <= geo.ntiles;
     uint32_t s = geo.in_state;
@@ -461,13 +509,18 @@ __global__ __launch_bounds__(HH_SCAN_TB) void k_scan1(Geometry geo, Work wk) {
             if (t < geo.emit_from) cnt = t + 1 == geo.emit_from ? hh_state_delta(hh_tab_state(row)) : 0;
         }
     }
+    // CONST seen in the prologue / in the emitted tiles: one atomic per
+    // block (one per wave on a single address serialises at the L2)
     const uint64_t mp = __ballot(cst && t < geo.emit_from), me = __ballot(cst && t >= geo.emit_from);
-    if ((threadIdx.x & 63u) == 0) {
-        if (mp) atomicOr(&wk.flags[12], 1u);
-        if (me) atomicOr(&wk.flags[13], 1u);
-    }
+    if (threadIdx.x == 0) s_cf = 0u;
+    __syncthreads();
+    if ((threadIdx.x & 63u) == 0 && (mp | me)) atomicOr(&s_cf, (mp ? 1u : 0u) | (me ? 2u : 0u));
     int32_t tot;
-    const int32_t ex = block_excl_scan<HH_SCAN_TB>(cnt, s_tmp, &tot);
+    const int32_t ex = block_excl_scan<HH_SCAN_TB>(cnt, s_tmp, &tot);   // (barriers inside)
+    if (threadIdx.x == 0) {
+        if (s_cf & 1u) atomicOr(&wk.flags[12], 1u);
+        if (s_cf & 2u) atomicOr(&wk.flags[13], 1u);
+    }
     if (valid) wk.lex[t] = ex;
     if (threadIdx.x == 0) wk.blk[blockIdx.x] = tot;
 }
@@ -508,36 +561,37 @@ __global__ __launch_bounds__(1024) void k_scan2(Geometry geo, Work wk, uint32_t 
 }
 
 // ---------------------------------------------------------------------------
-// k_emit: pass 2 of every emitted tile
+// k_emit: pass 2 of every emitted tile, in groups of HH_NW consecutive
+// tiles per workgroup (one tile per wave; the group's words, run offsets and
+// output staging are shared, each wave resolves its own tile's live lanes
+// from that tile's entering state).
 // ---------------------------------------------------------------------------
 template <uint32_t SW>
 __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__restrict__ gdata, Geometry geo,
                                                                DevTab tab, Work wk, uint8_t *__restrict__ out,
                                                                uint64_t cap) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ uint32_t s_ein[HH_NR];          // run entries pushed by walkers
-    __shared__ int16_t s_din[HH_NR];           // their deltas
-    __shared__ uint8_t s_k[HH_NR];
-    __shared__ uint8_t s_mem[HH_NR];
-    __shared__ uint16_t s_exc[HH_NR];
-    __shared__ uint32_t s_cnt[HH_NW];
+    __shared__ uint32_t s_ein[HH_GR];          // run entries pushed by walkers
+    __shared__ int16_t s_din[HH_GR];           // their deltas
+    __shared__ uint8_t s_k[HH_GR];
+    __shared__ uint8_t s_mem[HH_GR];
     __shared__ int32_t s_tmp[HH_NW];
 
     constexpr uint32_t S = 32 * SW;
     uint32_t *s_l1m = (uint32_t *)smem;
     uint32_t *s_l1s = s_l1m + HH_L1_SIZE;
-    uint32_t *s_w = s_l1s + HH_L1_SIZE;                 // SW * HH_NLS words (transposed)
-    uint32_t *s_out = s_w + SW * HH_NLS;                // HH_OB bytes of output staging
+    uint32_t *s_w = s_l1s + HH_L1_SIZE;                 // SW * HH_GNLS words (transposed)
+    uint32_t *s_out = s_w + SW * HH_GNLS;               // HH_OB bytes of output staging
     uint32_t *s_l2 = s_out + HH_OB / 4;
     uint32_t *s_tree = s_l2 + tab.l2_used;              // the compact tree (tail rule, long codes)
     uint8_t *s_tsym = (uint8_t *)(s_tree + tab.tree_lds);
 
-    const uint32_t j = threadIdx.x;
-    const uint64_t tile_bits = (uint64_t)HH_NR * S;
-    const uint32_t span = HH_NCOL * S;
+    const uint32_t j = threadIdx.x, jl = j & 63u, wv = j >> 6;
+    const uint64_t tile_bits = (uint64_t)HH_NR * S, group_bits = (uint64_t)HH_GR * S;
+    const uint32_t span = HH_GCOL * S;
     load_tables(tab, s_l1m, s_l1s, s_l2);
     // with the tree in LDS too, the decode loops issue no global load: a
-    // global load there would make them wait for the next tile's prefetch
+    // global load there would make them wait for the next group's prefetch
     for (uint32_t i = j; i < tab.tree_lds; i += HH_NL) {
         s_tree[i] = tab.tree[i];
         s_tsym[i] = tab.tsym[i];
@@ -546,6 +600,7 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     hh_ctx c;
     c.w = s_w;
     c.sw = SW;
+    c.nls = HH_GNLS;
     c.magic = 0;
     c.l1m = s_l1m;
     c.l1s = s_l1s;
@@ -555,77 +610,85 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     c.maxadv = geo.maxadv;
     c.G = geo.G;
 
-    // the next tile's words, lane record, entering state and output base are
-    // loaded one tile ahead (they are the loads every phase below waits on)
+    // Group g holds tiles f0 + HH_NW g + (0 .. HH_NW-1), f0 = emit_from.  The
+    // next group's words, lane records, entering states and output bases are
+    // loaded one group ahead (they are the loads every phase below waits
+    // on), the meta words BEFORE the words (vmcnt retires in order:
+    // consuming them then does not wait for the words).  The entering state
+    // and base are uniform per wave, but a uniform load is moved to an SGPR
+    // -- and waited for -- at once; so lanes 0..3 of every wave load one word
+    // each of the wave's tile (state, base low, base high, block-local
+    // prefix) and lanes 4..7 the same of the group's first tile; they are
+    // read out of those lanes only where the group consumes them.  Loads
+    // past the last tile read the last tile again (its wave emits nothing).
+    const uint64_t f0 = geo.emit_from;
+    const uint64_t ng = (geo.ntiles - f0 + HH_NW - 1) / HH_NW;   // (launched only when > 0)
+    const uint64_t tlast = geo.ntiles - 1;
     Prefetch pf;
     uint32_t rec_n = 0, meta_n = 0;
-    // Issued BEFORE the words (vmcnt retires in order: consuming them then
-    // does not wait for the words).  The tile's entering state and output
-    // base are uniform, but a uniform load is moved to an SGPR -- and waited
-    // for -- at once; so lanes 0..3 of every wave load one word each (state, base low,
-    // base high, block-local prefix) and the words are read out of lanes
-    // 0..3 only where the next tile consumes them.
-    auto prefetch_meta = [&](uint64_t tt) {
-        rec_n = wk.recs[tt * HH_NR + j];
+    auto prefetch_meta = [&](uint64_t g) {
+        const uint64_t tw = f0 + g * HH_NW + wv, tg = f0 + g * HH_NW;
+        const uint64_t tr = tw < tlast ? tw : tlast;
+        rec_n = wk.recs[tr * HH_NR + jl];
+        const uint32_t ln = jl & 3u;
+        const uint64_t tt = jl < 4 ? tr : tg;
         const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / HH_SCAN_TB);
-        const uint32_t ln = j & 63u;                    // (every wave reads its own copy)
         const uint32_t *src = ln == 0 ? &wk.st[tt] : ln == 1 ? blk32 : ln == 2 ? blk32 + 1
                                                                    : (const uint32_t *)&wk.lex[tt];
         meta_n = *src;
     };
-    uint64_t t = geo.emit_from + blockIdx.x;
-    if (t < geo.ntiles) {
-        prefetch_meta(t);
-        prefetch_tile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords, geo.vec4);
+    uint64_t g = blockIdx.x;
+    if (g < ng) {
+        prefetch_meta(g);
+        prefetch_group<SW>(pf, gdata, (f0 * tile_bits + g * group_bits) / 32, geo.nwords);
     }
-    for (; t < geo.ntiles; t += gridDim.x) {
-        __syncthreads();                                // previous tile's LDS no longer read
-        const uint64_t rem = geo.bits - t * tile_bits;
+    for (; g < ng; g += gridDim.x) {
+        __syncthreads();                                // previous group's LDS no longer read
+        const uint64_t t0 = f0 + g * HH_NW;             // the group's first tile
+        const bool wave_on = t0 + wv < geo.ntiles;
+        const uint64_t rem = geo.bits - t0 * tile_bits;
         c.bt = rem < span ? (uint32_t)rem : span;
         const uint32_t bt = c.bt;
-        store_tile<SW>(pf, s_w);
+        store_group<SW>(pf, s_w);
         const uint32_t rec = rec_n;
         // (readlane returns int: every word is cast to uint32_t before widening)
         const uint32_t st_in = (uint32_t)__builtin_amdgcn_readlane(meta_n, 0);
-        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane(meta_n, 1);
-        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane(meta_n, 2);
-        const int32_t lex_t = __builtin_amdgcn_readlane(meta_n, 3);
-        const int64_t base_t = (int64_t)(((uint64_t)bhi << 32) | blo) + (int64_t)lex_t;
-        const uint64_t tn = t + gridDim.x;
-        if (tn < geo.ntiles) {
-            prefetch_meta(tn);
-            prefetch_tile<SW>(pf, gdata, tn * tile_bits / 32, geo.nwords, geo.vec4);
+        const uint32_t st_g = (uint32_t)__builtin_amdgcn_readlane(meta_n, 4);
+        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane(meta_n, 5);
+        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane(meta_n, 6);
+        const int32_t lex_g = __builtin_amdgcn_readlane(meta_n, 7);
+        const int64_t base_g = (int64_t)(((uint64_t)bhi << 32) | blo) + (int64_t)lex_g;
+        const uint64_t gn = g + gridDim.x;
+        if (gn < ng) {
+            prefetch_meta(gn);
+            prefetch_group<SW>(pf, gdata, (f0 * tile_bits + gn * group_bits) / 32, geo.nwords);
         }
         const uint32_t kk = rec_k(rec), ee = rec_e(rec);
         const int32_t dl = rec_delta(rec);
-        resolve_live(kk, s_k, s_mem, s_exc, s_cnt);     // barriers inside (also publish s_w)
+        // live lanes of this wave's tile (walks never cover past the tile)
+        const uint32_t mem = resolve_live_wave(kk, s_k + 64 * wv, s_mem + 64 * wv);
 
         // the entering state: first live lane d_t, entered e_t bits in
         const uint32_t d_t = hh_state_d(st_in);
         const int32_t dprev = hh_state_delta(st_in);
-        const bool live = (s_mem[j] >> d_t) & 1u;
-        if (live && j + kk < HH_NR) {
+        const bool live = wave_on && ((mem >> d_t) & 1u);
+        if (live && jl + kk < HH_NR) {
             s_ein[j + kk] = (j + kk) * S + ee;
             s_din[j + kk] = (int16_t)dl;
         }
-        __syncthreads();
-        const uint32_t e_in = j == d_t ? d_t * S + hh_state_e(st_in) : s_ein[j];
-        const int32_t d_in = j == d_t ? dprev : (int32_t)s_din[j];
+        WAVE_SYNC();
+        const uint32_t e_in = jl == d_t ? (j - jl + d_t) * S + hh_state_e(st_in) : s_ein[j];
+        const int32_t d_in = jl == d_t ? dprev : (int32_t)s_din[j];
         const uint32_t rc = live ? (uint32_t)((int32_t)rec_nc(rec) + d_in) : 0u;
         int32_t Tout_i;
         const uint32_t L = (uint32_t)block_excl_scan<HH_NL>((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
         const uint32_t Tout = (uint32_t)Tout_i;
-        const int64_t P0s = base_t - (int64_t)dprev;
+        // the group's output starts where its first tile's does
+        const int64_t P0s = base_g - (int64_t)hh_state_delta(st_g);
         const uint64_t P0 = (uint64_t)P0s;
-        // the tile's output fits [0, cap) (no wrap-around)
+        // the group's output fits [0, cap) (no wrap-around)
         const bool fits = P0s >= 0 && P0 <= cap && Tout <= cap - P0;
         if (j == 0 && !fits) atomicOr(wk.flags, (uint32_t)F_OVER);
-#ifdef HH_DEBUG_OVER
-        if (j == 0 && !fits && atomicAdd(&wk.flags[4], 1u) == 0) {
-            wk.flags[5] = (uint32_t)t; wk.flags[6] = (uint32_t)P0; wk.flags[7] = (uint32_t)(P0 >> 32);
-            wk.flags[8] = Tout; wk.flags[9] = st_in;
-        }
-#endif
 
         hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
         const uint32_t y = (j + kk) * S + ee;
@@ -958,13 +1021,13 @@ static uint32_t pick_region_bits(const hh_tables *t, int req) {
         return (uint32_t)req;
     }
     uint32_t S = hh_pick_region_bits(g);
-    // A fixed-length code puts HH_NR * S / len symbols in every tile: keep
+    // A fixed-length code puts HH_GR * S / len symbols in every group: keep
     // that within k_emit's staging buffer (E.coli: 2-bit codes, S = 128).
     if (t->fixed_len > 0 && S) {
         uint32_t x = 32, y = g;
         while (y) { const uint32_t r = x % y; x = y; y = r; }
         const uint32_t lcm = 32 / x * g;
-        const uint64_t smax = (uint64_t)(HH_OB - 64) * (uint32_t)t->fixed_len / HH_NR;
+        const uint64_t smax = (uint64_t)(HH_OB - 64) * (uint32_t)t->fixed_len / HH_GR;
         while (S > smax && S > lcm) S -= lcm;
     }
     return S;
@@ -988,7 +1051,7 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     d->S = pick_region_bits(d->ht, d->cfg.lane_bits);
     d->G = hh_pick_overlap(d->ht);
     if (getenv("HH_OVERLAP")) d->G = (uint32_t)atoi(getenv("HH_OVERLAP")) & ~31u;   // experiments
-    if (d->G > 64 || d->G + 32 > d->S) d->G = 0;
+    if (d->G > HH_GMAX || d->G + 32 > d->S) d->G = 0;
     d->have_tree = 1;
     return HH_OK;
 }
@@ -1015,10 +1078,10 @@ static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8
                           uint64_t cap, uint64_t *out_len, hipStream_t st);
 
 static size_t lds_front(uint32_t sw, uint32_t l2) {
-    return ((size_t)HH_L1_SIZE + 2 * (size_t)sw * HH_NLS + l2) * 4;
+    return ((size_t)HH_L1_SIZE + ((l2 + 3) & ~3u) + (size_t)HH_NW * 2 * sw * HH_NLS) * 4;
 }
 static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree) {
-    return (2 * (size_t)HH_L1_SIZE + (size_t)sw * HH_NLS + l2) * 4 + HH_OB + (size_t)tree * 5;
+    return (2 * (size_t)HH_L1_SIZE + (size_t)sw * HH_GNLS + l2) * 4 + HH_OB + (size_t)tree * 5;
 }
 
 // kernels instantiated per words-per-region (S = 32 * SW bits)
@@ -1152,9 +1215,12 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     if (!kf || !ke) return HH_ERR_UNSUPPORTED;
     rc = size_grids(d, geo.sw);
     if (rc) return rc;
-    const uint32_t gf = (uint32_t)(nt < d->grid_f ? nt : d->grid_f);
+    // front: one tile per wave at a time; emit: groups of HH_NW tiles
+    const uint64_t nfw = (nt + HH_NW - 1) / HH_NW;
+    const uint32_t gf = (uint32_t)(nfw < d->grid_f ? nfw : d->grid_f);
     const uint64_t ne = nt > emit_from ? nt - emit_from : 0;
-    const uint32_t ge = (uint32_t)(ne < d->grid_e ? (ne ? ne : 1) : d->grid_e);
+    const uint64_t ng = (ne + HH_NW - 1) / HH_NW;
+    const uint32_t ge = (uint32_t)(ng < d->grid_e ? (ng ? ng : 1) : d->grid_e);
 
     HIP_OK(hipMemsetAsync(wk.flags, 0, 64, st));
 #ifdef HH_DIAG

@@ -48,7 +48,8 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
     if (S == 0) S = hh_pick_region_bits((uint32_t)T.len_gcd);
     stats[3] = S;
     uint32_t G = hh_pick_overlap(&T);
-    if (getenv("HH_EMU_G")) G = (uint32_t)atoi(getenv("HH_EMU_G"));
+    if (getenv("HH_EMU_G") && !T.fixed_len) G = (uint32_t)atoi(getenv("HH_EMU_G"));
+    if (G > HH_GMAX || G + 32 > S) G = 0;          // (the kernel's rule)
     if (leave) *leave = in_state;
     if (entry) *entry = in_state;
     if (bits == 0) return 0;
@@ -68,7 +69,7 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
         l1s[i] = (uint32_t)T.l1[i];
     }
     std::vector<uint32_t> mk((size_t)sw * HH_NLS);   // boundary masks (transposed like w)
-    std::vector<uint64_t> hd(HH_NR);                 // overlap heads (hh_region_head)
+    std::vector<hh_head> hd(HH_NR);                  // overlap heads (hh_region_head)
     std::vector<int32_t> din(HH_NR);
     std::vector<hh_wk> wk(HH_NR);
     stats[0] = (int64_t)ntiles;
@@ -94,6 +95,7 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
             for (uint32_t k = 0; k < sw; k++) w[k * HH_NLS + col] = word_at(tw0 + (uint64_t)col * sw + k);
         c.w = w.data();
         c.sw = sw;
+        c.nls = HH_NLS;
         c.magic = hh_magic(sw);
         c.l1m = l1m.data();
         c.l1s = l1s.data();
@@ -110,7 +112,7 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
             mk[i] = (uint32_t)(0x9e3779b9u * (uint32_t)(i + t * 7919u + 1));   // hold junk
         for (uint32_t j = 0; j < HH_NR; j++) {            // pass 1 (head, then count)
             uint32_t p0 = j * S, n = 0, x = bt, y = p0;
-            hd[j] = 0;
+            hd[j] = hh_head{0ull, 0ull};
             if (p0 < bt) {
                 if (j > 0 && G) y = hh_region_head(&c, p0 - G, p0, &hd[j]);
                 uint32_t lim = p0 + S < bt ? p0 + S : bt;
