@@ -340,27 +340,17 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
  * [s, R) as bits of *head (bit i <=> a symbol starts at s + i).  Pass 1 then
  * counts C_r from y, exactly as a chain started at y (so counts, masks and
  * walks keep the offset-0 semantics with R's entry point y instead of R). */
-#define HH_GMAX 128u          /* largest overlap */
-typedef struct {
-    uint64_t lo, hi;          /* boundary bits of [s, s + 128) */
-} hh_head;
-
-HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, hh_head *head) {
-    uint64_t lo = 0, hi = 0;
+#define HH_GMAX 64u           /* largest overlap */
+HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, uint64_t *head) {
+    uint64_t h = 0;
     hh_cur u = hh_cur_at(c, s);
     while (u.p < R && u.p < c->bt) {
         hh_look L = hh_lookup_w(c, u.p, hh_cur_win(u));
         const uint32_t o = hh_first_ge(L, R - u.p);     /* first start >= R, or nb */
-        const uint64_t v = L.bm & hh_lowmask(o);
-        const uint32_t off = u.p - s;                   /* < 128 */
-        lo |= off < 64 ? v << off : 0ull;
-        hi |= off >= 64 ? v << (off - 64) : off > 32 ? v >> (64 - off) : 0ull;
+        h |= (uint64_t)(L.bm & hh_lowmask(o)) << (u.p - s);
         hh_cur_adv(c, u, o);
     }
-    if (head) {
-        head->lo = lo;
-        head->hi = hi;
-    }
+    if (head) *head = h;
     return u.p < c->bt ? u.p : c->bt;
 }
 
@@ -369,15 +359,11 @@ HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, hh_head *
  * bits there meet C_{j+1}'s head bits: then the chains are identical from
  * that boundary on, C_j's exit is C_{j+1}'s entry point y, and the walk
  * from C_j's exit merges at once (k = 1, delta = 0). */
-HH_HD bool hh_window_merge(const hh_ctx *c, const uint32_t *mask, hh_head next, uint32_t R) {
-    uint64_t mlo = 0, mhi = 0;
-    const uint32_t g0 = (R - c->G) / 32 + 2;
-    for (uint32_t w = 0; w < c->G / 32; w++) {
-        const uint64_t v = mask[hh_idx(c, g0 + w)];
-        if (w < 2) mlo |= v << (32 * w);
-        else mhi |= v << (32 * (w - 2));
-    }
-    return ((mlo & next.lo) | (mhi & next.hi)) != 0;
+HH_HD bool hh_window_merge(const hh_ctx *c, const uint32_t *mask, uint64_t head_next, uint32_t R) {
+    uint64_t mine = 0;
+    for (uint32_t w = 0; w < c->G / 32; w++)
+        mine |= (uint64_t)mask[hh_idx(c, (R - c->G) / 32 + w + 2)] << (32 * w);
+    return (mine & head_next) != 0;
 }
 
 /* Symbols of a region's own chain that start before region offset off

@@ -295,10 +295,17 @@ __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, 
 #define DIAG_FLUSH(dbg) do { if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 6; i_++) atomicAdd((unsigned long long *)&(dbg)[i_], (unsigned long long)dg_acc[i_]); \
     if ((threadIdx.x & 63u) == 0) { for (int i_ = 0; i_ < 3; i_++) atomicAdd((unsigned long long *)&(dbg)[8 + i_], (unsigned long long)dg_w[i_]); \
         atomicMax((unsigned long long *)&(dbg)[11], (unsigned long long)dg_w[3]); } } while (0)
+#define EDIAG_DECL uint64_t eg_acc[5] = {0, 0, 0, 0, 0}; uint64_t eg_t = __builtin_amdgcn_s_memtime();
+#define EDIAG_STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); eg_acc[i] += t_ - eg_t; eg_t = t_; } while (0)
+#define EDIAG_FLUSH(dbg) do { if ((threadIdx.x & 63u) == 0) { const int ix_[5] = {6, 7, 12, 13, 14}; \
+    for (int i_ = 0; i_ < 5; i_++) atomicAdd((unsigned long long *)&(dbg)[ix_[i_]], (unsigned long long)eg_acc[i_]); } } while (0)
 #else
 #define DIAG_DECL
 #define DIAG_STAMP(i) do {} while (0)
 #define DIAG_FLUSH(dbg) do {} while (0)
+#define EDIAG_DECL
+#define EDIAG_STAMP(i) do {} while (0)
+#define EDIAG_FLUSH(dbg) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -374,7 +381,7 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
         // the own chain from its entry point y, counted and masked
         const uint32_t p0 = j * S;
         uint32_t n = 0, x = bt;
-        hh_head head = {0ull, 0ull};
+        uint64_t head = 0;
         if (p0 < bt) {
             const uint32_t y = j > 0 && c.G ? hh_region_head(&c, p0 - c.G, p0, &head) : p0;
             const uint32_t lim = p0 + S < bt ? p0 + S : bt;
@@ -388,15 +395,10 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
         // this chain's exit, no walk.  Its head comes from the next lane; the
         // last lane walks into the next tile (two pointers).
         const uint32_t R1 = (j + 1) * S;
-        auto shfl64 = [](uint64_t v) {
-            const uint32_t a = (uint32_t)__shfl_down((int)(uint32_t)v, 1, 64);
-            const uint32_t b = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1, 64);
-            return ((uint64_t)b << 32) | a;
-        };
-        hh_head nh;
-        nh.lo = shfl64(head.lo);
-        nh.hi = c.G > 64 ? shfl64(head.hi) : 0ull;
-        const bool merged = c.G && j != 63u && R1 < bt && hh_window_merge(&c, s_mk, nh, R1);
+        const uint32_t hlo = (uint32_t)__shfl_down((int)(uint32_t)head, 1, 64);
+        const uint32_t hhi = (uint32_t)__shfl_down((int)(uint32_t)(head >> 32), 1, 64);
+        const bool merged = c.G && j != 63u && R1 < bt &&
+                            hh_window_merge(&c, s_mk, ((uint64_t)hhi << 32) | hlo, R1);
 
         // walks: region j's exit against the next regions' own chains
         hh_wk w = {1u, x - R1, 0u, 0, 0u, 0u};
@@ -569,7 +571,7 @@ __global__ __launch_bounds__(1024) void k_scan2(Geometry geo, Work wk, uint32_t 
 template <uint32_t SW>
 __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__restrict__ gdata, Geometry geo,
                                                                DevTab tab, Work wk, uint8_t *__restrict__ out,
-                                                               uint64_t cap) {
+                                                               uint64_t cap, uint64_t *dbg) {
     extern __shared__ __align__(16) uint8_t smem[];
     __shared__ uint32_t s_ein[HH_GR];          // run entries pushed by walkers
     __shared__ int16_t s_din[HH_GR];           // their deltas
@@ -642,6 +644,7 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
         prefetch_meta(g);
         prefetch_group<SW>(pf, gdata, (f0 * tile_bits + g * group_bits) / 32, geo.nwords);
     }
+    EDIAG_DECL
     for (; g < ng; g += gridDim.x) {
         __syncthreads();                                // previous group's LDS no longer read
         const uint64_t t0 = f0 + g * HH_NW;             // the group's first tile
@@ -704,9 +707,11 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
 #else
         if (false) {
 #endif
+            EDIAG_STAMP(0);                             // (records, live lanes, scan)
             const uint32_t nq = (a0 + Tout + 15u) / 16u;
             for (uint32_t i = j; i < nq; i += HH_NL) *(u32x4 *)(s_out + 4 * i) = (u32x4){0u, 0u, 0u, 0u};
             __syncthreads();
+            EDIAG_STAMP(1);                             // (zeroing)
 #ifdef HH_EXP_NODEC
             if (false) {
 #else
@@ -750,13 +755,15 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
                 }
                 if (nacc) atomicOr(&s_out[wd], (uint32_t)acc);
             }
+            EDIAG_STAMP(2);                             // (own decode)
             __syncthreads();
+            EDIAG_STAMP(3);                             // (its barrier wait)
             uint8_t *gb = out + (P0 - a0);
             const uint8_t *sb = (const uint8_t *)s_out;
             for (uint32_t i = j; i < nq; i += HH_NL) {
                 const uint32_t lo = 16 * i;
                 if (lo >= a0 && lo + 16 <= a0 + Tout) {
-#ifdef HH_EXP_NT
+#ifndef HH_EXP_PLAIN_STORE
                     __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
 #else
                     *(u32x4 *)(gb + lo) = *(const u32x4 *)(sb + lo);
@@ -766,6 +773,7 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
                     for (uint32_t q = lo > a0 ? lo : a0; q < e; q++) gb[q] = sb[q];
                 }
             }
+            EDIAG_STAMP(4);                             // (copy-out)
             continue;
         }
         // a tile too large for the staging buffer: this lane's symbols
@@ -818,6 +826,7 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
             for (uint32_t i = 0; i < nacc; i++) ob[o + i] = (uint8_t)(acc >> (8 * i));
         }
     }
+    EDIAG_FLUSH(dbg);
 }
 
 // ---------------------------------------------------------------------------
@@ -906,7 +915,7 @@ __global__ void k_st_findmax(int64_t bits, const int32_t *idx, int32_t *maxv) {
 // Host side
 // ---------------------------------------------------------------------------
 typedef void (*kfront_t)(const uint32_t *, Geometry, DevTab, Work, uint64_t *);
-typedef void (*kemit_t)(const uint32_t *, Geometry, DevTab, Work, uint8_t *, uint64_t);
+typedef void (*kemit_t)(const uint32_t *, Geometry, DevTab, Work, uint8_t *, uint64_t, uint64_t *);
 
 struct hh_decoder {
     int device;
@@ -1238,7 +1247,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     HIP_OK(hipEventRecord(d->ev[2], st));
     if (ne) {
         hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds), st,
-                           (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap);
+                           (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap, d->d_dbg);
         HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(d->ev[3], st));
@@ -1250,7 +1259,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
         if (rc) return rc;
         if (ne) {
             hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds), st,
-                               (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap);
+                               (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap, d->d_dbg);
             HIP_OK(hipGetLastError());
         }
         HIP_OK(hipEventRecord(d->ev[3], st));

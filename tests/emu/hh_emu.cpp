@@ -69,7 +69,7 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
         l1s[i] = (uint32_t)T.l1[i];
     }
     std::vector<uint32_t> mk((size_t)sw * HH_NLS);   // boundary masks (transposed like w)
-    std::vector<hh_head> hd(HH_NR);                  // overlap heads (hh_region_head)
+    std::vector<uint64_t> hd(HH_NR);                 // overlap heads (hh_region_head)
     std::vector<int32_t> din(HH_NR);
     std::vector<hh_wk> wk(HH_NR);
     stats[0] = (int64_t)ntiles;
@@ -112,7 +112,7 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
             mk[i] = (uint32_t)(0x9e3779b9u * (uint32_t)(i + t * 7919u + 1));   // hold junk
         for (uint32_t j = 0; j < HH_NR; j++) {            // pass 1 (head, then count)
             uint32_t p0 = j * S, n = 0, x = bt, y = p0;
-            hd[j] = hh_head{0ull, 0ull};
+            hd[j] = 0;
             if (p0 < bt) {
                 if (j > 0 && G) y = hh_region_head(&c, p0 - G, p0, &hd[j]);
                 uint32_t lim = p0 + S < bt ? p0 + S : bt;
