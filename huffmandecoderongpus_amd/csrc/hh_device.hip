@@ -1,17 +1,18 @@
 // hh_device.hip -- HIP kernels (gfx950) and the device half of the C ABI.
 //
-// The decode is three launches on one stream, no in-kernel waits between
+// The decode is four launches on one stream, no in-kernel waits between
 // workgroups (O(N) memory, 64-bit offsets):
 //
-//   k_front   per tile of HH_NR regions x S bits, independent of every other
-//             tile (persistent grid, static tile stride):
+//   k_front   one tile (HH_NR = 64 regions x S bits) per WAVE at a time,
+//             persistent grid, independent of every other tile and wave:
 //               stage     the tile's words (+ the next tile's first HH_KM
 //                         regions and a halo), prefetched one tile ahead into
-//                         registers, stored to LDS transposed
-//               pass 1    every lane decodes its region from offset 0: count,
-//                         exit and boundary mask (decodeallbits)
-//               walks     each exit is walked against the next regions'
-//                         chains until they share a boundary (makebigtable)
+//                         registers, stored to the wave's LDS slice transposed
+//               pass 1    every lane decodes its region from a G-bit overlap
+//                         head: count, exit and boundary mask (decodeallbits)
+//               walks     each exit that did not merge in the overlap window
+//                         is walked against the next regions' chains until
+//                         they share a boundary (makebigtable)
 //               table     charged count and leaving state for every entering
 //                         state d < HH_KM -> workspace; one 32-bit record per
 //                         lane (regions crossed, entry offset, correction,
@@ -20,9 +21,10 @@
 //             composed through the tables back to the nearest CONST tile) and
 //             the exclusive prefix of the tiles' charged counts
 //             (calcbitsindex / findmax)
-//   k_emit    per tile, independent again: live lanes from the entering
-//             state, run offsets by a block scan, each lane re-decodes its
-//             exact run straight to HBM with dword stores (calcresult)
+//   k_emit    groups of HH_NW tiles per workgroup (one per wave): live lanes
+//             from each tile's entering state, run offsets by a block scan,
+//             each lane re-decodes its exact run into an LDS staging buffer,
+//             copied out with 16-B stores (calcresult)
 //
 // Reference-shaped stage kernels (k_st_*) mirror the six .cl kernels one by
 // one for intermediate-array parity.
