@@ -5,21 +5,25 @@ Workload (BASELINE.json configs[2]): a synthetic 1 GiB English-text .huff --
 kjv.txt tiled (about 349.4 copies) and encoded with the files/kjv.txt.huff
 codebook, cut at a symbol boundary -- decoded on each MI355X.  One "step" is
 one full decode of that stream with the input already resident in HBM:
-hh_decode_device (one k_decode launch: speculative region decode, walks,
-transfer tables, look-back, emission) plus its status readback.  For N > 1
-the stream is N GiB, sharded by whole tiles (weak scaling); each step is
-the rank's segment decode (with its prologue tiles) plus the entry-state
-exchange (one 5-integer all-gather); the decoded segments are all-gathered
-once after the timed region and reported separately (`allgather`).
+hh_decode_device (k_front: overlap heads, speculative region decode, walks,
+transfer tables; k_scan1/k_scan2: entering states and tile bases; k_emit:
+emission) plus its status readback.  For N > 1 the stream is N GiB, sharded
+by whole tiles (weak scaling); each step is the rank's segment decode (with
+its prologue tiles) plus the entry-state exchange (one 5-integer
+all-gather); the decoded segments are all-gathered once after the timed
+region and reported separately (`allgather`).
 
 Prints ONE JSON line on rank 0.  `roofline.achieved` = (C + D algorithmic
-bytes per decode) / the k_decode launch's average device time, measured with
-HIP events on the launch's stream inside the timed region; `traffic` is the
+bytes per decode) / the pipeline's average device time, measured with HIP
+events on the launches' stream inside the timed region; `traffic` is the
 HBM bytes per decode measured by rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-(profiles/pmc_latest.json, tools/gpu_profile.sh).  `cpu_baseline` times the
-reference's own linApproach (oracle/_ref, compiled from the reference's C
-sources) or, if that was not built, the oracle's restatement, on a bounded
-sample (kjv.txt.huff) on one host core.
+(profiles/pmc_latest.json, tools/profile.sh).  On one GPU the line also
+carries `workloads` (the E.coli-tiled and i.i.d. kjv-unigram streams of the
+same size) and `evaluate` (the reference's evaluate() scope:
+host payload in, host symbols out).  `cpu_baseline` times the reference's
+own linApproach (oracle/_ref, compiled from the reference's C sources) or,
+if that was not built, the oracle's restatement, on a bounded sample
+(kjv.txt.huff) on one host core.
 """
 from __future__ import annotations
 
