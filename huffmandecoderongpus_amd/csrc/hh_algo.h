@@ -108,6 +108,8 @@ typedef struct {
     const uint32_t *l1m;  /* HH_L1_SIZE entries: the meta half (bits 32..63
                              of the hh_internal.h L1 entry; HH_M_*)      */
     const uint32_t *l1s;  /* the symbol half (bits 0..31; escape: L2 ref) */
+    const uint64_t *l1;   /* or both halves interleaved (one 64-bit read per
+                             lookup; k_emit), null if split               */
     const uint32_t *l2;
     const uint32_t *tree; /* compact tree (tail symbols, very long codes) */
     const uint8_t *tsym;
@@ -211,7 +213,9 @@ typedef struct {
 } hh_look;
 
 HH_HD hh_look hh_lookup_w(const hh_ctx *c, uint32_t p, uint32_t win) {
-    const uint32_t m = c->l1m[win & (HH_L1_SIZE - 1u)];
+    const uint32_t ix = win & (HH_L1_SIZE - 1u);
+    const uint64_t e = c->l1 ? c->l1[ix] : 0ull;
+    const uint32_t m = c->l1 ? (uint32_t)(e >> 32) : c->l1m[ix];
     hh_look L;
     L.ns = HH_M_NSYM(m);
     if (L.ns) {
@@ -220,7 +224,7 @@ HH_HD hh_look hh_lookup_w(const hh_ctx *c, uint32_t p, uint32_t win) {
         L.len0 = HH_M_LEN0(m);
         /* the front kernel stages only the meta half (l1s null): it never
          * needs the symbol bytes */
-        L.syms = c->l1s ? c->l1s[win & (HH_L1_SIZE - 1u)] : 0u;
+        L.syms = c->l1 ? (uint32_t)e : c->l1s ? c->l1s[ix] : 0u;
     } else {
         uint32_t s;
         L.nb = L.len0 = hh_escape(c, p, win, m, &s);

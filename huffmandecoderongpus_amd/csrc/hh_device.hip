@@ -40,8 +40,12 @@
 #include "hiphuff.h"
 
 #define HH_MAXLEN_FAST 32           // longest code of the fast path (one cursor step <= 32 bits)
-#define HH_NL 256                   // lanes per workgroup (both kernels)
-#define HH_NW (HH_NL / 64)          // waves per workgroup
+#define HH_NL 256                   // lanes per workgroup (k_emit)
+#define HH_NW (HH_NL / 64)          // waves per workgroup (k_emit)
+#ifndef HH_FW
+#define HH_FW 4                     // waves per workgroup (k_front); 5 and 6 measured slower
+                                    // (a 5-wave workgroup puts two waves on one SIMD)
+#endif
 // k_emit works on groups of HH_NW consecutive tiles, one per wave, staged
 // together (one output staging buffer and one scan per group)
 #define HH_GR (HH_NW * HH_NR)       // regions per group
@@ -270,17 +274,17 @@ __device__ __forceinline__ uint32_t resolve_live_wave(uint32_t kk, uint8_t *s_k,
 
 // Decode tables into LDS (meta halves always; symbol halves when s_l1s).
 __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, uint32_t *s_l1s, uint32_t *s_l2) {
-    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += HH_NL) {
+    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += blockDim.x) {
         const uint64_t e = tab.l1[i];
         s_l1m[i] = (uint32_t)(e >> 32);
         if (s_l1s) s_l1s[i] = (uint32_t)e;
     }
-    for (uint32_t i = threadIdx.x; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
+    for (uint32_t i = threadIdx.x; i < tab.l2_used; i += blockDim.x) s_l2[i] = tab.l2[i];
 }
 
-#ifndef HH_FRONT_MINW
-#define HH_FRONT_MINW 5   // waves per SIMD the front kernel's registers are sized for (<= 96
-                          // VGPRs; its LDS also admits 5 workgroups per CU)
+#ifndef HH_FRONT_MINB
+#define HH_FRONT_MINB 4   // workgroups per CU the front kernel's registers are sized for: with
+                          // HH_FW = 5, 5 waves per SIMD (<= 96 VGPRs)
 #endif
 #ifndef HH_EMIT_MINW
 #define HH_EMIT_MINW 4
@@ -317,15 +321,15 @@ __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, 
 // slice, never with other waves: no workgroup barrier after the tables.
 // ---------------------------------------------------------------------------
 template <uint32_t SW>
-__global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *__restrict__ gdata, Geometry geo,
+__global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint32_t *__restrict__ gdata, Geometry geo,
                                                                  DevTab tab, Work wk, uint64_t *dbg) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ uint32_t s_xa[HH_NW][HH_NR];    // pass-1 exits
-    __shared__ uint16_t s_na[HH_NW][HH_NR];    // pass-1 counts
-    __shared__ uint8_t s_ka[HH_NW][HH_NR];
-    __shared__ uint8_t s_mema[HH_NW][HH_NR];
-    __shared__ int32_t s_cda[HH_NW][HH_KM];    // per-d counts of the partially live lanes
-    __shared__ uint32_t s_osta[HH_NW][HH_KM];  // per-d leaving states
+    __shared__ uint32_t s_xa[HH_FW][HH_NR];    // pass-1 exits
+    __shared__ uint16_t s_na[HH_FW][HH_NR];    // pass-1 counts
+    __shared__ uint8_t s_ka[HH_FW][HH_NR];
+    __shared__ uint8_t s_mema[HH_FW][HH_NR];
+    __shared__ int32_t s_cda[HH_FW][HH_KM];    // per-d counts of the partially live lanes
+    __shared__ uint32_t s_osta[HH_FW][HH_KM];  // per-d leaving states
 
     constexpr uint32_t S = 32 * SW;
     const uint32_t j = threadIdx.x & 63u, wv = threadIdx.x >> 6;
@@ -350,6 +354,7 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
     c.magic = 0;
     c.l1m = s_l1m;
     c.l1s = nullptr;
+    c.l1 = nullptr;
     c.l2 = s_l2;
     c.tree = tab.tree;
     c.tsym = tab.tsym;
@@ -361,11 +366,11 @@ __global__ __launch_bounds__(HH_NL, HH_FRONT_MINW) void k_front(const uint32_t *
     // stores: vmcnt retires in order and counts stores too).  The loads run
     // unconditionally (the last tile again past the end): a conditional load
     // merges two values, which the compiler waits for.
-    const uint64_t nwv = (uint64_t)gridDim.x * HH_NW;
+    const uint64_t nwv = (uint64_t)gridDim.x * HH_FW;
     const uint64_t tlast = geo.ntiles ? geo.ntiles - 1 : 0;
     auto clampt = [&](uint64_t tt) { return tt < tlast ? tt : tlast; };
     Prefetch pf;
-    uint64_t t = (uint64_t)blockIdx.x * HH_NW + wv;
+    uint64_t t = (uint64_t)blockIdx.x * HH_FW + wv;
     if (t < geo.ntiles) {
         prefetch_wtile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords);
         store_wtile<SW>(pf, s_w);
@@ -582,9 +587,9 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     __shared__ int32_t s_tmp[HH_NW];
 
     constexpr uint32_t S = 32 * SW;
-    uint32_t *s_l1m = (uint32_t *)smem;
-    uint32_t *s_l1s = s_l1m + HH_L1_SIZE;
-    uint32_t *s_w = s_l1s + HH_L1_SIZE;                 // SW * HH_GNLS words (transposed)
+    uint64_t *s_l1 = (uint64_t *)smem;                  // L1 entries as in global memory: one
+                                                        // 64-bit read gives meta and symbols
+    uint32_t *s_w = (uint32_t *)(s_l1 + HH_L1_SIZE);    // SW * HH_GNLS words (transposed)
     uint32_t *s_out = s_w + SW * HH_GNLS;               // HH_OB bytes of output staging
     uint32_t *s_l2 = s_out + HH_OB / 4;
     uint32_t *s_tree = s_l2 + tab.l2_used;              // the compact tree (tail rule, long codes)
@@ -593,7 +598,8 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     const uint32_t j = threadIdx.x, jl = j & 63u, wv = j >> 6;
     const uint64_t tile_bits = (uint64_t)HH_NR * S, group_bits = (uint64_t)HH_GR * S;
     const uint32_t span = HH_GCOL * S;
-    load_tables(tab, s_l1m, s_l1s, s_l2);
+    for (uint32_t i = j; i < HH_L1_SIZE; i += HH_NL) s_l1[i] = tab.l1[i];
+    for (uint32_t i = j; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
     // with the tree in LDS too, the decode loops issue no global load: a
     // global load there would make them wait for the next group's prefetch
     for (uint32_t i = j; i < tab.tree_lds; i += HH_NL) {
@@ -606,8 +612,9 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     c.sw = SW;
     c.nls = HH_GNLS;
     c.magic = 0;
-    c.l1m = s_l1m;
-    c.l1s = s_l1s;
+    c.l1 = s_l1;
+    c.l1m = nullptr;
+    c.l1s = nullptr;
     c.l2 = s_l2;
     c.tree = s_tree;                                    // (fast_path_ok: the tree fits)
     c.tsym = s_tsym;
@@ -726,8 +733,9 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
                 while (cu.p < pf_end) {            // whole lookups
                     const uint32_t win = hh_cur_win(cu);
                     const uint32_t ix = win & (HH_L1_SIZE - 1u);
-                    const uint32_t m = c.l1m[ix];
-                    uint32_t sy = c.l1s[ix], ns = HH_M_NSYM(m), nb = HH_M_NBITS(m);
+                    const uint64_t le = s_l1[ix];
+                    const uint32_t m = (uint32_t)(le >> 32);
+                    uint32_t sy = (uint32_t)le, ns = HH_M_NSYM(m), nb = HH_M_NBITS(m);
                     if (ns == 0) {
                         nb = hh_escape(&c, cu.p, win, m, &sy);
                         ns = 1;
@@ -798,8 +806,9 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
             while (cu.p < pf_end) {
                 const uint32_t win = hh_cur_win(cu);
                 const uint32_t ix = win & (HH_L1_SIZE - 1u);
-                const uint32_t m = c.l1m[ix];
-                uint32_t sy = c.l1s[ix], ns = HH_M_NSYM(m), nb = HH_M_NBITS(m);
+                const uint64_t le = s_l1[ix];
+                const uint32_t m = (uint32_t)(le >> 32);
+                uint32_t sy = (uint32_t)le, ns = HH_M_NSYM(m), nb = HH_M_NBITS(m);
                 if (ns == 0) {
                     nb = hh_escape(&c, cu.p, win, m, &sy);
                     ns = 1;
@@ -1089,7 +1098,7 @@ static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8
                           uint64_t cap, uint64_t *out_len, hipStream_t st);
 
 static size_t lds_front(uint32_t sw, uint32_t l2) {
-    return ((size_t)HH_L1_SIZE + ((l2 + 3) & ~3u) + (size_t)HH_NW * 2 * sw * HH_NLS) * 4;
+    return ((size_t)HH_L1_SIZE + ((l2 + 3) & ~3u) + (size_t)HH_FW * 2 * sw * HH_NLS) * 4;
 }
 static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree) {
     return (2 * (size_t)HH_L1_SIZE + (size_t)sw * HH_GNLS + l2) * 4 + HH_OB + (size_t)tree * 5;
@@ -1119,7 +1128,7 @@ static int size_grids(hh_decoder *d, uint32_t sw) {
     if (d->grid_f && d->grid_sw == sw && d->grid_l2 == d->tab.l2_used && d->grid_tree == d->tab.tree_lds)
         return HH_OK;
     int pf = 0, pe = 0, ncu = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pf, kfront_for(sw), HH_NL, lds_front(sw, d->tab.l2_used)));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pf, kfront_for(sw), 64 * HH_FW, lds_front(sw, d->tab.l2_used)));
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kemit_for(sw), HH_NL, lds_emit(sw, d->tab.l2_used, d->tab.tree_lds)));
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
     if (pf < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
@@ -1227,7 +1236,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     rc = size_grids(d, geo.sw);
     if (rc) return rc;
     // front: one tile per wave at a time; emit: groups of HH_NW tiles
-    const uint64_t nfw = (nt + HH_NW - 1) / HH_NW;
+    const uint64_t nfw = (nt + HH_FW - 1) / HH_FW;
     const uint32_t gf = (uint32_t)(nfw < d->grid_f ? nfw : d->grid_f);
     const uint64_t ne = nt > emit_from ? nt - emit_from : 0;
     const uint64_t ng = (ne + HH_NW - 1) / HH_NW;
@@ -1238,7 +1247,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     HIP_OK(hipMemsetAsync(d->d_dbg, 0, 16 * sizeof(uint64_t), st));
 #endif
     HIP_OK(hipEventRecord(d->ev[0], st));
-    hipLaunchKernelGGL(kf, dim3(gf), dim3(HH_NL), lds_front(geo.sw, d->tab.l2_used), st,
+    hipLaunchKernelGGL(kf, dim3(gf), dim3(64 * HH_FW), lds_front(geo.sw, d->tab.l2_used), st,
                        (const uint32_t *)d_data, geo, d->tab, wk, d->d_dbg);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d->ev[1], st));

@@ -99,6 +99,7 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
         c.magic = hh_magic(sw);
         c.l1m = l1m.data();
         c.l1s = l1s.data();
+        c.l1 = nullptr;
         c.l2 = T.l2;
         c.tree = T.tree;
         c.tsym = T.tsym;
