@@ -841,6 +841,92 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
 }
 
 // ---------------------------------------------------------------------------
+// Segment path: exact and O(N) for any code of at most 32 bits, whether or
+// not it resynchronises (the fast path's walks need it to).  The stream is
+// cut into segments of `seglen` bits.  The chain through a segment is fixed
+// by the offset o in [0, maxadv) of its first boundary past the segment
+// start, so k_seg_func decodes every segment from every o (one lane each):
+// the exit offset into the next segment and the symbols starting in the
+// segment.  The host composes the maps from segment 0 (offset 0): entry
+// offsets and output bases.  k_seg_emit re-decodes every segment from its
+// true entry (one lane each) straight to HBM.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void seg_ctx(hh_ctx &c, const uint32_t *gdata, uint64_t seg0, uint64_t bits,
+                                        uint32_t seglen, const uint32_t *s_l1m, const DevTab &tab,
+                                        uint32_t maxadv) {
+    c.w = gdata + seg0 / 32;                            // linear words of the segment:
+    c.sw = 1;                                           // hh_idx(g) == g
+    c.nls = 1;
+    c.magic = 0;
+    c.l1m = s_l1m;
+    c.l1s = nullptr;
+    c.l1 = nullptr;
+    c.l2 = tab.l2;
+    c.tree = tab.tree;
+    c.tsym = tab.tsym;
+    c.maxadv = maxadv;
+    c.G = 0;
+    const uint64_t rem = bits - seg0;
+    const uint64_t lim = (uint64_t)seglen + 2 * maxadv;
+    c.bt = (uint32_t)(rem < lim ? rem : lim);
+}
+
+__global__ __launch_bounds__(256) void k_seg_func(const uint32_t *__restrict__ gdata, uint64_t bits,
+                                                  uint32_t seglen, uint32_t nseg, uint32_t no,
+                                                  DevTab tab, uint32_t maxadv, uint32_t *exits,
+                                                  uint32_t *counts) {
+    __shared__ uint32_t s_l1m[HH_L1_SIZE];
+    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += blockDim.x) s_l1m[i] = (uint32_t)(tab.l1[i] >> 32);
+    __syncthreads();
+    const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (id >= (uint64_t)nseg * no) return;
+    const uint32_t sg = (uint32_t)(id / no), o = (uint32_t)(id % no);
+    const uint64_t seg0 = (uint64_t)sg * seglen;
+    hh_ctx c;
+    seg_ctx(c, gdata, seg0, bits, seglen, s_l1m, tab, maxadv);
+    const uint32_t end = c.bt < seglen ? c.bt : seglen;  // symbols starting before it count
+    uint32_t n = 0, x = o;
+    if (o < end) x = hh_region_count(&c, o, end, &n);
+    exits[id] = x >= end ? x - end : 0u;                // offset into the next segment
+    counts[id] = n;
+}
+
+__global__ __launch_bounds__(256) void k_seg_emit(const uint32_t *__restrict__ gdata, uint64_t bits,
+                                                  uint32_t seglen, uint32_t nseg, DevTab tab,
+                                                  uint32_t maxadv, const uint32_t *entry,
+                                                  const uint32_t *exitv, const uint64_t *base,
+                                                  uint8_t *__restrict__ out) {
+    __shared__ uint32_t s_l1m[HH_L1_SIZE];
+    __shared__ uint32_t s_l1s[HH_L1_SIZE];
+    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += blockDim.x) {
+        const uint64_t e = tab.l1[i];
+        s_l1m[i] = (uint32_t)(e >> 32);
+        s_l1s[i] = (uint32_t)e;
+    }
+    __syncthreads();
+    const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sg >= nseg) return;
+    const uint64_t seg0 = (uint64_t)sg * seglen;
+    hh_ctx c;
+    seg_ctx(c, gdata, seg0, bits, seglen, s_l1m, tab, maxadv);
+    c.l1s = s_l1s;
+    const uint32_t end = c.bt < seglen ? c.bt : seglen;
+    const uint32_t e0 = entry[sg];
+    // the run ends at the first boundary at or past the segment end (or bt)
+    const uint32_t pe0 = end + exitv[sg], pe = pe0 < c.bt ? pe0 : c.bt;
+    if (e0 >= end) return;
+    uint8_t *ob = out + base[sg];
+    hh_cur cu = hh_cur_at(&c, e0);
+    uint64_t o = 0;
+    uint32_t val, k;
+    while (cu.p < pe) {
+        hh_emit_step(&c, cu, pe, o, ~0ull, &val, &k);
+        for (uint32_t i = 0; i < k; i++) ob[o + i] = (uint8_t)(val >> (8 * i));
+        o += k;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Reference-shaped stage kernels (ReleaseCL/kernels/ *.cl, one each).
 // ---------------------------------------------------------------------------
 __global__ void k_st_init(int32_t *idx, int64_t bits) {
@@ -1091,7 +1177,7 @@ static inline unsigned grid_for(int64_t n, unsigned bs) {
 
 static int fast_path_ok(const hh_decoder *d) {
     return d->S >= 32 && d->S <= 32 * HH_SW_MAX && d->ht->maxlen <= HH_MAXLEN_FAST &&
-           d->ht->tree_used <= HH_TREE_LDS_MAX && !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
+           d->ht->tree_used <= HH_TREE_LDS_MAX && !(d->cfg.flags & (HH_FLAG_FORCE_EXACT | HH_FLAG_FORCE_SEGMENT));
 }
 
 static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8_t *d_out,
@@ -1300,6 +1386,67 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     return HH_OK;
 }
 
+// The segment path (above).  Memory: 8 bytes per (segment, offset) and 16
+// per segment; the maps are composed on the host.
+static int segment_path(hh_decoder *d, const void *d_data, uint64_t bits, uint8_t *d_out, uint64_t cap,
+                        uint64_t *out_len, hipStream_t st) {
+    const uint32_t maxadv = d->ht->maxlen > HH_P ? (uint32_t)d->ht->maxlen : HH_P;
+    const uint32_t no = (uint32_t)d->ht->maxlen;        // boundary offsets past a segment start
+    const uint32_t seglen = 1u << 16;
+    const uint64_t nseg64 = (bits + seglen - 1) / seglen;
+    if (nseg64 > 0xffffffffull / no) return HH_ERR_UNSUPPORTED;
+    const uint32_t nseg = (uint32_t)nseg64;
+    const size_t nmap = (size_t)nseg * no;
+    uint32_t *dm = nullptr;
+    uint64_t *dbase = nullptr;
+    uint32_t *hx = (uint32_t *)malloc(nmap * 8), *hent = (uint32_t *)malloc((size_t)nseg * 8);
+    uint64_t *hbase = (uint64_t *)malloc((size_t)nseg * 8);
+    int rc = HH_OK;
+    if (!hx || !hent || !hbase) { rc = HH_ERR_NOMEM; goto out; }
+    if (hipMalloc(&dm, nmap * 8 + (size_t)nseg * 8) != hipSuccess || hipMalloc(&dbase, (size_t)nseg * 8) != hipSuccess) {
+        rc = HH_ERR_NOMEM;
+        goto out;
+    }
+    {
+        uint32_t *dexit = dm, *dcnt = dm + nmap;
+        const uint64_t nl = nmap;
+        hipLaunchKernelGGL(k_seg_func, dim3((unsigned)((nl + 255) / 256)), dim3(256), 0, st,
+                           (const uint32_t *)d_data, bits, seglen, nseg, no, d->tab, maxadv, dexit, dcnt);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpyAsync(hx, dm, nmap * 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) { rc = HH_ERR_DEVICE; goto out; }
+        const uint32_t *hexit = hx, *hcnt = hx + nmap;
+        uint32_t o = 0;
+        uint64_t run = 0;
+        for (uint32_t sg = 0; sg < nseg; sg++) {
+            if (o >= no) { rc = HH_ERR_INTERNAL; goto out; }
+            hent[sg] = o;
+            hent[nseg + sg] = hexit[(size_t)sg * no + o];
+            hbase[sg] = run;
+            run += hcnt[(size_t)sg * no + o];
+            o = hent[nseg + sg];
+        }
+        *out_len = run;
+        if (run > cap) { rc = HH_ERR_CAPACITY; goto out; }
+        uint32_t *dent = dm;                            // (the maps are no longer needed)
+        if (hipMemcpyAsync(dent, hent, (size_t)nseg * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(dbase, hbase, (size_t)nseg * 8, hipMemcpyHostToDevice, st) != hipSuccess) {
+            rc = HH_ERR_DEVICE;
+            goto out;
+        }
+        hipLaunchKernelGGL(k_seg_emit, dim3((nseg + 255) / 256), dim3(256), 0, st, (const uint32_t *)d_data,
+                           bits, seglen, nseg, d->tab, maxadv, dent, dent + nseg, dbase, d_out);
+        if (hipGetLastError() != hipSuccess || hipStreamSynchronize(st) != hipSuccess) rc = HH_ERR_DEVICE;
+    }
+out:
+    if (dm) hipFree(dm);
+    if (dbase) hipFree(dbase);
+    free(hx);
+    free(hent);
+    free(hbase);
+    return rc;
+}
+
 extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits, void *d_out,
                                 uint64_t cap, uint64_t *out_len, void *hip_stream) {
     if (!d || !out_len || (!d_data && bits) || (!d_out && cap)) return HH_ERR_ARG;
@@ -1312,7 +1459,12 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     memset(&d->stats, 0, sizeof(d->stats));
     *out_len = 0;
     if (bits == 0) return HH_OK;
-    if (!fast_path_ok(d)) {
+    const bool seg_ok = d->ht->maxlen <= HH_MAXLEN_FAST && !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
+    if (!fast_path_ok(d) || (d->cfg.flags & HH_FLAG_FORCE_SEGMENT)) {
+        if (seg_ok) {
+            d->stats.exact_fallback = 2;
+            return segment_path(d, d_data, bits, (uint8_t *)d_out, cap, out_len, st);
+        }
         d->stats.exact_fallback = 1;
         return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
     }
@@ -1322,10 +1474,10 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
                          &leave, &cp, &cs, &en);
     if (rc == HH_ERR_UNSUPPORTED) {
         // A walk found no shared boundary within HH_KM regions (a code that
-        // does not resynchronise): take the reference-shaped stage pipeline.
-        d->stats.exact_fallback = 1;
+        // does not resynchronise): the segment path, exact and O(N).
+        d->stats.exact_fallback = 2;
         d->stats.repairs = 1;
-        return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
+        return segment_path(d, d_data, bits, (uint8_t *)d_out, cap, out_len, st);
     }
     *out_len = total;
     return rc;

@@ -129,6 +129,10 @@ typedef struct {
                                    reference-shaped stage pipeline (the six
                                    hh_stage_* kernels: exact, O(25 * bits)
                                    memory, bits < 2^31) */
+#define HH_FLAG_FORCE_SEGMENT 2 /* skip the fast path and decode with the
+                                   segment path (exact, O(N), any length;
+                                   the path codes that do not resynchronise
+                                   take, codes <= 32 bits) */
 
 int hh_decoder_create(hh_decoder **dec, const hh_config *cfg);
 void hh_decoder_destroy(hh_decoder *dec);
@@ -148,9 +152,10 @@ typedef struct {
     uint64_t lanes;          /* lane regions                                 */
     uint64_t repairs;        /* 1: a tile-state chain was composed on the
                                 host (or the stage pipeline ran)            */
-    int exact_fallback;      /* 1 if the stage pipeline decoded (a code the
-                                fast path does not take, or a walk that
-                                found no merge)                             */
+    int exact_fallback;      /* 0: the fast path decoded; 1: the stage
+                                pipeline (codes longer than 32 bits); 2: the
+                                segment path (a walk found no merge: a code
+                                that does not resynchronise)                */
 } hh_stats;
 
 int hh_decoder_stats(const hh_decoder *dec, hh_stats *st);

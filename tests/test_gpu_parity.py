@@ -450,3 +450,69 @@ def test_shard_job_two_ranks_one_gpu():
         assert ok is True, (rank, ok)
         assert n > 0
     assert got[1][3] > 0          # rank 1 decoded a prologue
+
+
+@pytest.mark.parametrize("name", ["hello", "paper1", "news", "kjv.txt", "E.coli"])
+def test_segment_path_fixtures(hh, files_dir, name):
+    """The segment path (HH_FLAG_FORCE_SEGMENT), byte-exact on the fixtures."""
+    path = os.path.join(files_dir, name + ".huff")
+    hf = hh.HuffFile.load(path)
+    ref = O.OracleHuff.load(path).chain_decode()
+    dec = hh.Decoder(0, flags=2)
+    try:
+        dec.set_tree(hf.tree())
+        out = dec.decode_host(hf.payload, hf.bits, hf.uncompressedsize + 3)
+        assert dec.stats()["exact_fallback"] == 2
+        assert np.array_equal(out, ref)
+    finally:
+        dec.close()
+
+
+def test_non_resynchronising_code_takes_the_segment_path(hh):
+    """An 11-bit fixed-length code with 96-bit regions realigns only every 11
+    regions (> HH_KM): the walks fail and the decoder must switch to the
+    exact O(N) segment path, not mis-decode."""
+    iz, io, sy = _complete_tree(11)
+    rng = np.random.default_rng(11)
+    bits = 11 * 300000 + 5
+    data = rng.integers(0, 256, size=bits // 8 + 1).astype(np.uint8)
+    ref = _oracle(iz, io, sy, data, bits)
+    dec = hh.Decoder(0, lane_bits=96)
+    try:
+        dec.set_tree(hh.Tree(iz, io, sy))
+        got = _decode_dev(hh, dec, data, bits, bits)
+        assert dec.stats()["exact_fallback"] == 2
+        assert len(got) == len(ref) and np.array_equal(got, ref)
+    finally:
+        dec.close()
+
+
+def test_non_resynchronising_code_beyond_2_31_bits(hh):
+    """The same code on a 2.2e9-bit stream (past the stage pipeline's int32
+    cap): 200 M random symbols encoded on the GPU, decoded by the segment
+    path, compared with the symbols."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    iz, io, sy = _complete_tree(11)
+    tree = hh.Tree(iz, io, sy)
+    code, lens = synth.code_table(tree)
+    n = 200_000_000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    syms = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    payload, bits = synth.encode_gpu(syms, code, lens)
+    assert bits == 11 * n and bits > 1 << 31
+    dec = hh.Decoder(0, lane_bits=96)
+    try:
+        dec.set_tree(tree)
+        out = torch.full((n + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+        got = dec.decode_device(payload, bits, out)
+        torch.cuda.synchronize()
+        assert dec.stats()["exact_fallback"] == 2
+        assert got == n
+        assert torch.equal(out[:n], syms)
+        assert int(out[n:n + 64].ne(0xAB).sum()) == 0
+    finally:
+        dec.close()
+        del out, payload, syms
+        torch.cuda.empty_cache()
