@@ -1,5 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 --timeout-method thread -k "segment or resynchronising" > gpurun_out/t_seg.log 2>&1 || exit 1
-timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "not eight_shards and not hufx" > gpurun_out/t.log 2>&1 || exit 1
+export HH_TEXT_CACHE=$GRAFT_REPO_ROOT/gpurun_out/text_kjv.txt.npy
+rm -f $HH_TEXT_CACHE
+timeout -k 10 120 python3 tools/time_lib.py 1 1 kjv.txt 2>>gpurun_out/ab.err || exit 1
+HH_FLAGS=2 timeout -k 10 300 python3 tools/time_lib.py 1024 3 kjv.txt > gpurun_out/seg.log 2>>gpurun_out/ab.err || exit 1

@@ -37,13 +37,18 @@ dec = H.Decoder(0, flags=int(os.environ.get("HH_FLAGS", "0")))
 dec.set_tree(syn.tree)
 out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device="cuda")
 ph = {"total": [], "sync": [], "scan": [], "emit": []}
+wall = []
 ok = True
 for i in range(reps + 1):
+    import time
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     try:
         n = dec.decode_device(syn.data, syn.bits, out)
     except H.HipHuffError:          # experiment variants (wrong counts by design)
         n = -1
     torch.cuda.synchronize()
+    wall.append((time.perf_counter() - t0) * 1e3)
     if i == 0:
         ok = n == syn.decoded_bytes and synth.verify_tiled(out, syn)
         continue
@@ -53,6 +58,7 @@ for i in range(reps + 1):
 res = {"lib": os.path.basename(os.environ.get("HIPHUFF_LIB", H.LIB_PATH)), "mib": mib, "src": src,
        "ok": bool(ok), "fast": dec.stats()["exact_fallback"] == 0}
 res.update({k: round(statistics.median(v), 4) for k, v in ph.items()})
+res["wall_ms"] = round(statistics.median(wall[1:]), 3)
 if os.environ.get("HH_DIAG"):            # a -DHH_DIAG build: phase cycles and walk lengths
     import ctypes as C
     buf = (C.c_uint64 * 16)()
