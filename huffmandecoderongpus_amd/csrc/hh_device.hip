@@ -21,9 +21,9 @@
 //             composed through the tables back to the nearest CONST tile) and
 //             the exclusive prefix of the tiles' charged counts
 //             (calcbitsindex / findmax)
-//   k_emit    groups of HH_NW tiles per workgroup (one per wave): live lanes
-//             from each tile's entering state, run offsets by a block scan,
-//             each lane re-decodes its exact run into an LDS staging buffer,
+//   k_emit    one tile per WAVE at a time again: live lanes from the tile's
+//             entering state, run offsets by a wave scan, each lane
+//             re-decodes its exact run into the wave's LDS staging buffer,
 //             copied out with 16-B stores (calcresult)
 //
 // Reference-shaped stage kernels (k_st_*) mirror the six .cl kernels one by
@@ -46,15 +46,10 @@
 #define HH_FW 4                     // waves per workgroup (k_front); 5 and 6 measured slower
                                     // (a 5-wave workgroup puts two waves on one SIMD)
 #endif
-// k_emit works on groups of HH_NW consecutive tiles, one per wave, staged
-// together (one output staging buffer and one scan per group)
-#define HH_GR (HH_NW * HH_NR)       // regions per group
-#define HH_GCOL (HH_GR + HH_KM + 1) // staged columns
-#define HH_GNLS 288                 // their column stride (>= HH_GCOL, multiple of 32)
 #define HH_SCAN_TB 1024             // tiles per k_scan1 block
 #define HH_SCAN_BACK 4096           // longest non-CONST chain k_scan1 composes (else host scan)
-#define HH_OB (16384 + 64)          // k_emit's LDS output staging (bytes): a text group's output
-                                    // (<= ~15.2 K symbols for kjv) plus the 16-B phase
+#define HH_OBW (4096 + 64)          // k_emit's LDS output staging per wave (bytes): a text tile's
+                                    // output (~3.7 K symbols for kjv) plus the 16-B phase
 
 #define HIP_OK(x)                                                             \
     do {                                                                      \
@@ -186,19 +181,17 @@ __device__ __forceinline__ void load_region(uint32_t *v, __amdgpu_buffer_rsrc_t 
     }
 }
 
-// Registers holding one tile's (k_front) or group's (k_emit) words for this
-// lane: its region column and up to two words of the columns past the span
-// (the next tile's first HH_KM regions and the halo).
+// Registers holding one tile's words for this lane: its region column and up
+// to two words of the columns past the tile (the next tile's first HH_KM
+// regions and the halo).
 static_assert((HH_NCOL - HH_NR) * HH_SW_MAX <= 2 * 64, "a tile's extra columns: two words per lane");
-static_assert((HH_GCOL - HH_GR) * HH_SW_MAX <= HH_NL, "a group's extra columns: one word per lane");
-static_assert(HH_NLS >= HH_NCOL && HH_NLS % 16 == 0 && HH_GNLS >= HH_GCOL && HH_GNLS % 32 == 0,
-              "LDS column strides");
+static_assert(HH_NLS >= HH_NCOL && HH_NLS % 16 == 0, "LDS column stride");
 struct Prefetch {
     uint32_t v[HH_SW_MAX];
     uint32_t halo, halo2;
 };
 
-// k_front: a wave's tile (lane = its region)
+// a wave's tile (lane = its region)
 template <uint32_t sw>
 __device__ __forceinline__ void prefetch_wtile(Prefetch &pf, const uint32_t *g, uint64_t tw0, uint64_t nok) {
     const uint32_t j = threadIdx.x & 63u;
@@ -217,24 +210,6 @@ __device__ __forceinline__ void store_wtile(const Prefetch &pf, uint32_t *s_w) {
         if (k < sw) s_w[k * HH_NLS + j] = pf.v[k];
     if (j < nx) s_w[(j % sw) * HH_NLS + HH_NR + j / sw] = pf.halo;
     if (j + 64 < nx) s_w[((j + 64) % sw) * HH_NLS + HH_NR + (j + 64) / sw] = pf.halo2;
-}
-
-// k_emit: a workgroup's group of tiles (lane = its region within the group)
-template <uint32_t sw>
-__device__ __forceinline__ void prefetch_group(Prefetch &pf, const uint32_t *g, uint64_t tw0, uint64_t nok) {
-    const uint32_t j = threadIdx.x;
-    const __amdgpu_buffer_rsrc_t r = words_rsrc(g, tw0, nok);
-    load_region<sw>(pf.v, r, j);
-    constexpr uint32_t nx = (HH_GCOL - HH_GR) * sw;
-    pf.halo = j < nx ? __builtin_amdgcn_raw_buffer_load_b32(r, (int)(4u * (HH_GR * sw + j)), 0, 0) : 0u;
-}
-template <uint32_t sw>
-__device__ __forceinline__ void store_group(const Prefetch &pf, uint32_t *s_w) {
-    const uint32_t j = threadIdx.x;
-#pragma unroll
-    for (uint32_t k = 0; k < HH_SW_MAX; k++)
-        if (k < sw) s_w[k * HH_GNLS + j] = pf.v[k];
-    if (j < (HH_GCOL - HH_GR) * sw) s_w[(j % sw) * HH_GNLS + HH_GR + j / sw] = pf.halo;
 }
 
 // Lanes of one wave exchanging values through LDS: a wave's LDS operations
@@ -570,47 +545,49 @@ __global__ __launch_bounds__(1024) void k_scan2(Geometry geo, Work wk, uint32_t 
 }
 
 // ---------------------------------------------------------------------------
-// k_emit: pass 2 of every emitted tile, in groups of HH_NW consecutive
-// tiles per workgroup (one tile per wave; the group's words, run offsets and
-// output staging are shared, each wave resolves its own tile's live lanes
-// from that tile's entering state).
+// k_emit: pass 2 of every emitted tile, one tile per wave at a time (wave gw
+// takes tiles f0 + gw, f0 + gw + #waves, ...; f0 = emit_from).  Like
+// k_front, a wave never waits for another: its tile's words, live lanes,
+// run offsets (a wave scan) and output staging are its own.
 // ---------------------------------------------------------------------------
 template <uint32_t SW>
 __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__restrict__ gdata, Geometry geo,
                                                                DevTab tab, Work wk, uint8_t *__restrict__ out,
                                                                uint64_t cap, uint64_t *dbg) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ uint32_t s_ein[HH_GR];          // run entries pushed by walkers
-    __shared__ int16_t s_din[HH_GR];           // their deltas
-    __shared__ uint8_t s_k[HH_GR];
-    __shared__ uint8_t s_mem[HH_GR];
-    __shared__ int32_t s_tmp[HH_NW];
+    __shared__ uint32_t s_eina[HH_NW][HH_NR];  // run entries pushed by walkers
+    __shared__ int16_t s_dina[HH_NW][HH_NR];   // their deltas
+    __shared__ uint8_t s_ka[HH_NW][HH_NR];
+    __shared__ uint8_t s_mema[HH_NW][HH_NR];
 
     constexpr uint32_t S = 32 * SW;
+    const uint32_t j = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint64_t *s_l1 = (uint64_t *)smem;                  // L1 entries as in global memory: one
                                                         // 64-bit read gives meta and symbols
-    uint32_t *s_w = (uint32_t *)(s_l1 + HH_L1_SIZE);    // SW * HH_GNLS words (transposed)
-    uint32_t *s_out = s_w + SW * HH_GNLS;               // HH_OB bytes of output staging
-    uint32_t *s_l2 = s_out + HH_OB / 4;
+    uint32_t *s_out = (uint32_t *)(s_l1 + HH_L1_SIZE) + wv * (HH_OBW / 4);   // the wave's staging
+    uint32_t *s_w = (uint32_t *)(s_l1 + HH_L1_SIZE) + HH_NW * (HH_OBW / 4) + wv * (SW * HH_NLS);
+    uint32_t *s_l2 = (uint32_t *)(s_l1 + HH_L1_SIZE) + HH_NW * (HH_OBW / 4 + SW * HH_NLS);
     uint32_t *s_tree = s_l2 + tab.l2_used;              // the compact tree (tail rule, long codes)
     uint8_t *s_tsym = (uint8_t *)(s_tree + tab.tree_lds);
+    uint32_t *s_ein = s_eina[wv];
+    int16_t *s_din = s_dina[wv];
 
-    const uint32_t j = threadIdx.x, jl = j & 63u, wv = j >> 6;
-    const uint64_t tile_bits = (uint64_t)HH_NR * S, group_bits = (uint64_t)HH_GR * S;
-    const uint32_t span = HH_GCOL * S;
-    for (uint32_t i = j; i < HH_L1_SIZE; i += HH_NL) s_l1[i] = tab.l1[i];
-    for (uint32_t i = j; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
+    const uint64_t tile_bits = (uint64_t)HH_NR * S;
+    const uint32_t span = HH_NCOL * S;
+    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += HH_NL) s_l1[i] = tab.l1[i];
+    for (uint32_t i = threadIdx.x; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
     // with the tree in LDS too, the decode loops issue no global load: a
-    // global load there would make them wait for the next group's prefetch
-    for (uint32_t i = j; i < tab.tree_lds; i += HH_NL) {
+    // global load there would make them wait for the next tile's prefetch
+    for (uint32_t i = threadIdx.x; i < tab.tree_lds; i += HH_NL) {
         s_tree[i] = tab.tree[i];
         s_tsym[i] = tab.tsym[i];
     }
+    __syncthreads();                                    // (the only workgroup barrier)
 
     hh_ctx c;
     c.w = s_w;
     c.sw = SW;
-    c.nls = HH_GNLS;
+    c.nls = HH_NLS;
     c.magic = 0;
     c.l1 = s_l1;
     c.l1m = nullptr;
@@ -621,111 +598,87 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     c.maxadv = geo.maxadv;
     c.G = geo.G;
 
-    // Group g holds tiles f0 + HH_NW g + (0 .. HH_NW-1), f0 = emit_from.  The
-    // next group's words, lane records, entering states and output bases are
-    // loaded one group ahead (they are the loads every phase below waits
-    // on), the meta words BEFORE the words (vmcnt retires in order:
-    // consuming them then does not wait for the words).  The entering state
-    // and base are uniform per wave, but a uniform load is moved to an SGPR
-    // -- and waited for -- at once; so lanes 0..3 of every wave load one word
-    // each of the wave's tile (state, base low, base high, block-local
-    // prefix) and lanes 4..7 the same of the group's first tile; they are
-    // read out of those lanes only where the group consumes them.  Loads
-    // past the last tile read the last tile again (its wave emits nothing).
+    // The next tile's words, lane record, entering state and output base are
+    // loaded one tile ahead (they are the loads every phase below waits on),
+    // the meta words BEFORE the words (vmcnt retires in order: consuming them
+    // then does not wait for the words).  The entering state and base are
+    // uniform, but a uniform load is moved to an SGPR -- and waited for -- at
+    // once; so lanes 0..3 load one word each (state, base low, base high,
+    // block-local prefix), read out of those lanes where consumed.  Loads run
+    // unconditionally, past the last tile on the last tile again.
     const uint64_t f0 = geo.emit_from;
-    const uint64_t ng = (geo.ntiles - f0 + HH_NW - 1) / HH_NW;   // (launched only when > 0)
-    const uint64_t tlast = geo.ntiles - 1;
+    const uint64_t nwv = (uint64_t)gridDim.x * HH_NW;
+    const uint64_t tlast = geo.ntiles - 1;              // (launched only when f0 < ntiles)
+    auto clampt = [&](uint64_t tt) { return tt < tlast ? tt : tlast; };
     Prefetch pf;
     uint32_t rec_n = 0, meta_n = 0;
-    auto prefetch_meta = [&](uint64_t g) {
-        const uint64_t tw = f0 + g * HH_NW + wv, tg = f0 + g * HH_NW;
-        const uint64_t tr = tw < tlast ? tw : tlast;
-        rec_n = wk.recs[tr * HH_NR + jl];
-        const uint32_t ln = jl & 3u;
-        const uint64_t tt = jl < 4 ? tr : tg;
+    auto prefetch_next = [&](uint64_t tt) {
+        rec_n = wk.recs[tt * HH_NR + j];
         const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / HH_SCAN_TB);
+        const uint32_t ln = j & 3u;
         const uint32_t *src = ln == 0 ? &wk.st[tt] : ln == 1 ? blk32 : ln == 2 ? blk32 + 1
                                                                    : (const uint32_t *)&wk.lex[tt];
         meta_n = *src;
+        prefetch_wtile<SW>(pf, gdata, tt * tile_bits / 32, geo.nwords);
     };
-    uint64_t g = blockIdx.x;
-    if (g < ng) {
-        prefetch_meta(g);
-        prefetch_group<SW>(pf, gdata, (f0 * tile_bits + g * group_bits) / 32, geo.nwords);
-    }
+    uint64_t t = f0 + (uint64_t)blockIdx.x * HH_NW + wv;
+    if (t < geo.ntiles) prefetch_next(t);
     EDIAG_DECL
-    for (; g < ng; g += gridDim.x) {
-        __syncthreads();                                // previous group's LDS no longer read
-        const uint64_t t0 = f0 + g * HH_NW;             // the group's first tile
-        const bool wave_on = t0 + wv < geo.ntiles;
-        const uint64_t rem = geo.bits - t0 * tile_bits;
+    for (; t < geo.ntiles; t += nwv) {
+        WAVE_SYNC();                                    // the previous tile's LDS no longer read
+        const uint64_t rem = geo.bits - t * tile_bits;
         c.bt = rem < span ? (uint32_t)rem : span;
         const uint32_t bt = c.bt;
-        store_group<SW>(pf, s_w);
+        store_wtile<SW>(pf, s_w);
         const uint32_t rec = rec_n;
         // (readlane returns int: every word is cast to uint32_t before widening)
         const uint32_t st_in = (uint32_t)__builtin_amdgcn_readlane(meta_n, 0);
-        const uint32_t st_g = (uint32_t)__builtin_amdgcn_readlane(meta_n, 4);
-        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane(meta_n, 5);
-        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane(meta_n, 6);
-        const int32_t lex_g = __builtin_amdgcn_readlane(meta_n, 7);
-        const int64_t base_g = (int64_t)(((uint64_t)bhi << 32) | blo) + (int64_t)lex_g;
-        const uint64_t gn = g + gridDim.x;
-        if (gn < ng) {
-            prefetch_meta(gn);
-            prefetch_group<SW>(pf, gdata, (f0 * tile_bits + gn * group_bits) / 32, geo.nwords);
-        }
+        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane(meta_n, 1);
+        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane(meta_n, 2);
+        const int32_t lex_t = __builtin_amdgcn_readlane(meta_n, 3);
+        const int64_t base_t = (int64_t)(((uint64_t)bhi << 32) | blo) + (int64_t)lex_t;
+        prefetch_next(clampt(t + nwv));
         const uint32_t kk = rec_k(rec), ee = rec_e(rec);
         const int32_t dl = rec_delta(rec);
-        // live lanes of this wave's tile (walks never cover past the tile)
-        const uint32_t mem = resolve_live_wave(kk, s_k + 64 * wv, s_mem + 64 * wv);
+        const uint32_t mem = resolve_live_wave(kk, s_ka[wv], s_mema[wv]);
 
         // the entering state: first live lane d_t, entered e_t bits in
         const uint32_t d_t = hh_state_d(st_in);
         const int32_t dprev = hh_state_delta(st_in);
-        const bool live = wave_on && ((mem >> d_t) & 1u);
-        if (live && jl + kk < HH_NR) {
+        const bool live = (mem >> d_t) & 1u;
+        if (live && j + kk < HH_NR) {
             s_ein[j + kk] = (j + kk) * S + ee;
             s_din[j + kk] = (int16_t)dl;
         }
         WAVE_SYNC();
-        const uint32_t e_in = jl == d_t ? (j - jl + d_t) * S + hh_state_e(st_in) : s_ein[j];
-        const int32_t d_in = jl == d_t ? dprev : (int32_t)s_din[j];
+        const uint32_t e_in = j == d_t ? d_t * S + hh_state_e(st_in) : s_ein[j];
+        const int32_t d_in = j == d_t ? dprev : (int32_t)s_din[j];
         const uint32_t rc = live ? (uint32_t)((int32_t)rec_nc(rec) + d_in) : 0u;
-        int32_t Tout_i;
-        const uint32_t L = (uint32_t)block_excl_scan<HH_NL>((int32_t)rc, s_tmp, &Tout_i);   // barriers inside
-        const uint32_t Tout = (uint32_t)Tout_i;
-        // the group's output starts where its first tile's does
-        const int64_t P0s = base_g - (int64_t)hh_state_delta(st_g);
+        const int32_t incl = wave_incl_scan((int32_t)rc);
+        const uint32_t L = (uint32_t)incl - rc;
+        const uint32_t Tout = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+        const int64_t P0s = base_t - (int64_t)dprev;
         const uint64_t P0 = (uint64_t)P0s;
-        // the group's output fits [0, cap) (no wrap-around)
+        // the tile's output fits [0, cap) (no wrap-around)
         const bool fits = P0s >= 0 && P0 <= cap && Tout <= cap - P0;
         if (j == 0 && !fits) atomicOr(wk.flags, (uint32_t)F_OVER);
 
         hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
         const uint32_t y = (j + kk) * S + ee;
         const uint32_t pe = (live && fits) ? (y < bt ? y : bt) : 0u;
-        // The tile's output [P0, P0 + Tout) is staged in LDS at byte a0 =
-        // P0 mod 16, so that 16-B blocks of LDS and of HBM line up: lanes
-        // OR their symbols in as dwords (a dword two runs share needs the
-        // OR; the buffer is zeroed first), then the block copies it out with
-        // whole 16-B stores -- every line written once, by one instruction.
+        // The tile's output [P0, P0 + Tout) is staged in the wave's LDS at
+        // byte a0 = P0 mod 16, so that 16-B blocks of LDS and of HBM line
+        // up: lanes OR their symbols in as dwords (a dword two runs share
+        // needs the OR; the buffer is zeroed first), then the wave copies it
+        // out with whole 16-B stores -- every line written once.
         const uint32_t a0 = (uint32_t)(P0 & 15u);
-#ifndef HH_NO_STAGE
-        if (fits && a0 + Tout <= HH_OB) {
-#else
-        if (false) {
-#endif
+        if (fits && a0 + Tout <= HH_OBW) {
             EDIAG_STAMP(0);                             // (records, live lanes, scan)
             const uint32_t nq = (a0 + Tout + 15u) / 16u;
-            for (uint32_t i = j; i < nq; i += HH_NL) *(u32x4 *)(s_out + 4 * i) = (u32x4){0u, 0u, 0u, 0u};
-            __syncthreads();
+            for (uint32_t i = j; i < nq; i += 64) *(u32x4 *)(s_out + 4 * i) = (u32x4){0u, 0u, 0u, 0u};
+            WAVE_SYNC();
             EDIAG_STAMP(1);                             // (zeroing)
-#ifdef HH_EXP_NODEC
-            if (false) {
-#else
             if (cu.p < pe) {
-#endif
                 const uint32_t b = a0 + L;
                 uint32_t wd = b >> 2, nacc = b & 3u, emitted = 0, val, k;
                 uint64_t acc = 0;
@@ -766,11 +719,10 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
                 if (nacc) atomicOr(&s_out[wd], (uint32_t)acc);
             }
             EDIAG_STAMP(2);                             // (own decode)
-            __syncthreads();
-            EDIAG_STAMP(3);                             // (its barrier wait)
+            WAVE_SYNC();
             uint8_t *gb = out + (P0 - a0);
             const uint8_t *sb = (const uint8_t *)s_out;
-            for (uint32_t i = j; i < nq; i += HH_NL) {
+            for (uint32_t i = j; i < nq; i += 64) {
                 const uint32_t lo = 16 * i;
                 if (lo >= a0 && lo + 16 <= a0 + Tout) {
 #ifndef HH_EXP_PLAIN_STORE
@@ -1127,13 +1079,13 @@ static uint32_t pick_region_bits(const hh_tables *t, int req) {
         return (uint32_t)req;
     }
     uint32_t S = hh_pick_region_bits(g);
-    // A fixed-length code puts HH_GR * S / len symbols in every group: keep
+    // A fixed-length code puts HH_NR * S / len symbols in every tile: keep
     // that within k_emit's staging buffer (E.coli: 2-bit codes, S = 128).
     if (t->fixed_len > 0 && S) {
         uint32_t x = 32, y = g;
         while (y) { const uint32_t r = x % y; x = y; y = r; }
         const uint32_t lcm = 32 / x * g;
-        const uint64_t smax = (uint64_t)(HH_OB - 64) * (uint32_t)t->fixed_len / HH_GR;
+        const uint64_t smax = (uint64_t)(HH_OBW - 64) * (uint32_t)t->fixed_len / HH_NR;
         while (S > smax && S > lcm) S -= lcm;
     }
     return S;
@@ -1187,7 +1139,8 @@ static size_t lds_front(uint32_t sw, uint32_t l2) {
     return ((size_t)HH_L1_SIZE + ((l2 + 3) & ~3u) + (size_t)HH_FW * 2 * sw * HH_NLS) * 4;
 }
 static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree) {
-    return (2 * (size_t)HH_L1_SIZE + (size_t)sw * HH_GNLS + l2) * 4 + HH_OB + (size_t)tree * 5;
+    return (2 * (size_t)HH_L1_SIZE + (size_t)HH_NW * sw * HH_NLS + l2) * 4 + (size_t)HH_NW * HH_OBW +
+           (size_t)tree * 5;
 }
 
 // kernels instantiated per words-per-region (S = 32 * SW bits)
@@ -1321,11 +1274,11 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     if (!kf || !ke) return HH_ERR_UNSUPPORTED;
     rc = size_grids(d, geo.sw);
     if (rc) return rc;
-    // front: one tile per wave at a time; emit: groups of HH_NW tiles
+    // one tile per wave at a time in both kernels
     const uint64_t nfw = (nt + HH_FW - 1) / HH_FW;
     const uint32_t gf = (uint32_t)(nfw < d->grid_f ? nfw : d->grid_f);
     const uint64_t ne = nt > emit_from ? nt - emit_from : 0;
-    const uint64_t ng = (ne + HH_NW - 1) / HH_NW;
+    const uint64_t ng = (ne + HH_NW - 1) / HH_NW;          // workgroups' worth of tiles
     const uint32_t ge = (uint32_t)(ng < d->grid_e ? (ng ? ng : 1) : d->grid_e);
 
     HIP_OK(hipMemsetAsync(wk.flags, 0, 64, st));
