@@ -73,6 +73,11 @@
 #define HH_SW_MAX 12          /* max words per region (S <= 384) */
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
                                  as a failed walk) */
+#ifndef HH_FRONT_WALK
+#define HH_FRONT_WALK 16      /* lookups of a walk in k_front; longer walks are
+                                 deferred to k_walk (a wave would wait for its
+                                 longest walk) */
+#endif
 
 HH_HD uint32_t hh_umulhi(uint32_t a, uint32_t b) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -100,7 +105,7 @@ HH_HD uint32_t hh_lowmask(uint32_t o) { return o >= 32 ? 0xffffffffu : ((1u << o
 
 HH_HD uint32_t hh_magic(uint32_t sw) { return (uint32_t)((0x100000000ull + sw - 1) / sw); }
 
-typedef struct {
+typedef struct hh_ctx {
     const uint32_t *w;    /* transposed tile words                        */
     uint32_t sw;          /* words per region                             */
     uint32_t nls;         /* column stride of the staged words            */
@@ -119,6 +124,12 @@ typedef struct {
     uint32_t G;           /* overlap: region r's chain starts G bits before
                              the region (r > 0 within a tile), 0 or a
                              multiple of 32 <= 64 (see hh_region_head)   */
+    /* the front's table (hh_internal.h F), used by every lookup when pf is
+     * HH_PF (k_front, k_walk: no symbol bytes) -- then maxadv must cover
+     * HH_PF too */
+    const uint16_t *f = nullptr;
+    const uint32_t *fdir = nullptr;
+    uint32_t pf = 0;
 } hh_ctx;
 
 /* The kernel is instantiated per words-per-region (the kernel's hh_ctx has
@@ -213,6 +224,25 @@ typedef struct {
 } hh_look;
 
 HH_HD hh_look hh_lookup_w(const hh_ctx *c, uint32_t p, uint32_t win) {
+    if (c->pf) {                                   /* the front's table */
+        const uint32_t e = c->f[win & ((1u << c->pf) - 1u)];
+        hh_look L;
+        L.syms = 0;
+        L.nb = e & 15u;
+        if (L.nb) {
+            const uint32_t r = (e >> 4) << 1;
+            L.bm = r | 1u;
+            L.ns = hh_popc(L.bm);
+            L.len0 = r ? hh_ctz(r) : L.nb;
+        } else {
+            uint32_t s;
+            L.nb = L.len0 = hh_escape(c, p, win, c->fdir[e >> 4], &s);
+            L.ns = 1;
+            L.bm = 1;
+            L.syms = s;
+        }
+        return L;
+    }
     const uint32_t ix = win & (HH_L1_SIZE - 1u);
     const uint64_t e = c->l1 ? c->l1[ix] : 0ull;
     const uint32_t m = c->l1 ? (uint32_t)(e >> 32) : c->l1m[ix];
@@ -295,13 +325,27 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
     const uint32_t lf = lim > c->maxadv ? lim - c->maxadv : 0u;
     while (u.p < lf) {
         const uint32_t win = hh_cur_win(u);
-        const uint32_t m = c->l1m[win & (HH_L1_SIZE - 1u)];
-        uint32_t ns = HH_M_NSYM(m), nb = HH_M_NBITS(m), bm = HH_M_BMASK(m);
-        if (ns == 0) {
-            uint32_t s;
-            nb = hh_escape(c, u.p, win, m, &s);
-            ns = 1;
-            bm = 1;
+        uint32_t ns, nb, bm;
+        if (c->pf) {
+            const uint32_t e = c->f[win & ((1u << c->pf) - 1u)];
+            nb = e & 15u;
+            bm = ((e >> 4) << 1) | 1u;
+            ns = hh_popc(bm);
+            if (nb == 0) {
+                uint32_t s;
+                nb = hh_escape(c, u.p, win, c->fdir[e >> 4], &s);
+                ns = 1;
+                bm = 1;
+            }
+        } else {
+            const uint32_t m = c->l1m[win & (HH_L1_SIZE - 1u)];
+            ns = HH_M_NSYM(m), nb = HH_M_NBITS(m), bm = HH_M_BMASK(m);
+            if (ns == 0) {
+                uint32_t s;
+                nb = hh_escape(c, u.p, win, m, &s);
+                ns = 1;
+                bm = 1;
+            }
         }
         n += ns;
         if (mask) {
@@ -398,7 +442,11 @@ HH_HD uint32_t hh_mask_rank(const hh_ctx *c, const uint32_t *mask, uint32_t R, u
  *   e     W's first boundary in the merge region, as an offset from its start
  *   cov   W's symbols from x up to that boundary (the covered regions)
  *   delta W's symbols from there to the merge minus C's symbols before it
- * mask/xs/ns (may be null): masks, exits and counts of regions < nmask. */
+ * mask/xs/ns (may be null): masks, exits and counts of regions < nmask.
+ * ys (may be null): entry points y of the own chains of regions < nys (the
+ * pass-1 heads), so that two-pointer walks need not decode the heads again.
+ * maxit < HH_WALK_MAX bounds the lookups: a walk cut there returns more = 1
+ * (the front kernel defers it to k_walk, which walks again from x). */
 typedef struct {
     uint32_t k, e, cov;
     int32_t delta;
@@ -409,7 +457,8 @@ typedef struct {
 HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
                     const uint32_t *mask = nullptr, const uint32_t *xs = nullptr,
                     const uint16_t *ns = nullptr, uint32_t nmask = 0,
-                    uint32_t maxit = HH_WALK_MAX) {
+                    uint32_t maxit = HH_WALK_MAX, const uint32_t *ys = nullptr,
+                    uint32_t nys = 0) {
     hh_wk r = {0u, 0u, 0u, 0, 0u, 0u};
     const uint32_t bt = c->bt;
     uint32_t A = x < bt ? x : bt;
@@ -481,7 +530,8 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
             /* the region's own chain, entered at its entry point: the
              * next tile's region 0 starts at R, the others G bits early */
             uint32_t B = R < bt ? R : bt;
-            if (c->G && rg > nmask && R < bt) B = hh_region_head(c, R - c->G, R, nullptr);
+            if (rg < nys) B = ys[rg] < bt ? ys[rg] : bt;
+            else if (c->G && rg % HH_NR != 0 && R < bt) B = hh_region_head(c, R - c->G, R, nullptr);
             int32_t cb = 0;
             for (; it < maxit; it++) {
                 if (A == B) {

@@ -67,6 +67,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 struct DevTab {
     const uint64_t *l1;
+    const uint16_t *f;   // the front's table (hh_internal.h F) and its escape directory
+    const uint32_t *fdir;
+    uint32_t fdir_used;
     const uint32_t *l2;
     const uint32_t *tree;
     const uint8_t *tsym;
@@ -104,6 +107,9 @@ struct Geometry {
     uint32_t in_state;   // state entering tile 0 (a shard's entry; 0 at the stream start)
     uint64_t emit_from;  // tiles before this one are a prologue: decoded for their
                          // leaving state only (a shard's probe of its predecessor)
+    uint32_t fwalk;      // lookups of a walk in k_front (longer: deferred to k_walk)
+    uint32_t nfw;        // k_front's waves (each with its list of deferred walks)
+    uint64_t qcap;       // entries per list (the wave's tiles x HH_NR)
 };
 
 // Workspace carve (decode_fast).  Nothing but `flags` needs zeroing: every
@@ -115,6 +121,8 @@ struct Work {
     uint32_t *st;        // [ntiles + 1] state entering each tile (st[ntiles]: leaving the last)
     int32_t *lex;        // [ntiles + 1] exclusive prefix of charged counts within its scan block
     int64_t *blk;        // [nblk] scan block totals, then exclusive block bases
+    uint32_t *q;         // [nfw][qcap] deferred walks of each k_front wave (tile * HH_NR + lane)
+    uint32_t *qn;        // [nfw] their counts
 };
 
 // ---------------------------------------------------------------------------
@@ -250,6 +258,17 @@ __device__ __forceinline__ uint32_t resolve_live_wave(uint32_t kk, uint8_t *s_k,
     return s_mem[j];
 }
 
+// The front's tables into LDS: F, its escape directory, L2.
+__device__ __forceinline__ void load_ftables(const DevTab &tab, uint16_t *s_f, uint32_t *s_fdir, uint32_t *s_l2) {
+    const uint32_t *f32 = (const uint32_t *)tab.f;
+    for (uint32_t i = threadIdx.x; i < HH_F_SIZE / 2; i += blockDim.x) ((uint32_t *)s_f)[i] = f32[i];
+    for (uint32_t i = threadIdx.x; i < tab.fdir_used; i += blockDim.x) s_fdir[i] = tab.fdir[i];
+    for (uint32_t i = threadIdx.x; i < tab.l2_used; i += blockDim.x) s_l2[i] = tab.l2[i];
+}
+__host__ __device__ constexpr uint32_t ftab_words(uint32_t fdir, uint32_t l2) {
+    return HH_F_SIZE / 2 + ((fdir + 3u) & ~3u) + ((l2 + 3u) & ~3u);
+}
+
 // Decode tables into LDS (meta halves always; symbol halves when s_l1s).
 __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, uint32_t *s_l1s, uint32_t *s_l2) {
     for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += blockDim.x) {
@@ -293,36 +312,31 @@ __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, 
 #endif
 
 // ---------------------------------------------------------------------------
-// k_front: pass 1, walks and the transfer table of every tile, one tile per
-// wave at a time (a persistent grid; wave gw takes tiles gw, gw + #waves,
-// ...).  Within a tile the lanes exchange values through the wave's own LDS
-// slice, never with other waves: no workgroup barrier after the tables.
+// k_front: pass 1 and the short walks of every tile, one tile per wave at a
+// time (a persistent grid; wave gw takes tiles gw, gw + #waves, ...).  Within
+// a tile the lanes exchange values through the wave's own LDS slice, never
+// with other waves: no workgroup barrier after the tables.  A walk longer
+// than geo.fwalk lookups is deferred to k_walk (a wave would otherwise wait
+// for its longest walk: kjv's average walk is 0.5 lookups, a wave's longest
+// 16); the tables follow from the records in k_table.
 // ---------------------------------------------------------------------------
 template <uint32_t SW>
 __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint32_t *__restrict__ gdata, Geometry geo,
                                                                  DevTab tab, Work wk, uint64_t *dbg) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ uint32_t s_xa[HH_FW][HH_NR];    // pass-1 exits
-    __shared__ uint16_t s_na[HH_FW][HH_NR];    // pass-1 counts
-    __shared__ uint8_t s_ka[HH_FW][HH_NR];
-    __shared__ uint8_t s_mema[HH_FW][HH_NR];
-    __shared__ int32_t s_cda[HH_FW][HH_KM];    // per-d counts of the partially live lanes
-    __shared__ uint32_t s_osta[HH_FW][HH_KM];  // per-d leaving states
+    __shared__ uint32_t s_ya[HH_FW][HH_NR];    // entry points of the regions' own chains
 
     constexpr uint32_t S = 32 * SW;
     const uint32_t j = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    uint32_t *s_l1m = (uint32_t *)smem;                 // L1 meta halves (shared)
-    uint32_t *s_l2 = s_l1m + HH_L1_SIZE;                // L2 (shared), then the waves' slices:
-    uint32_t *s_w = s_l2 + ((tab.l2_used + 3u) & ~3u) + wv * (2 * SW * HH_NLS);   // SW * HH_NLS words
-    uint32_t *s_mk = s_w + SW * HH_NLS;                 // SW * HH_NLS boundary-mask words
-    uint32_t *s_x = s_xa[wv];
-    uint16_t *s_n = s_na[wv];
-    int32_t *s_cd = s_cda[wv];
-    uint32_t *s_ost = s_osta[wv];
+    uint16_t *s_f = (uint16_t *)smem;                   // F, its escape directory, L2 (shared),
+    uint32_t *s_fdir = (uint32_t *)smem + HH_F_SIZE / 2;
+    uint32_t *s_l2 = s_fdir + ((tab.fdir_used + 3u) & ~3u);
+    uint32_t *s_w = (uint32_t *)smem + ftab_words(tab.fdir_used, tab.l2_used) + wv * (SW * HH_NLS);
+    uint32_t *s_y = s_ya[wv];                           // then the waves' slices (SW * HH_NLS words)
 
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
     const uint32_t span = HH_NCOL * S;                  // bits staged per tile
-    load_tables(tab, s_l1m, nullptr, s_l2);
+    load_ftables(tab, s_f, s_fdir, s_l2);
     __syncthreads();                                    // (the only workgroup barrier)
 
     hh_ctx c;
@@ -330,13 +344,16 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
     c.sw = SW;
     c.nls = HH_NLS;
     c.magic = 0;
-    c.l1m = s_l1m;
+    c.l1m = nullptr;
     c.l1s = nullptr;
     c.l1 = nullptr;
+    c.f = s_f;
+    c.fdir = s_fdir;
+    c.pf = HH_PF;
     c.l2 = s_l2;
     c.tree = tab.tree;
     c.tsym = tab.tsym;
-    c.maxadv = geo.maxadv;
+    c.maxadv = geo.maxadv > HH_PF ? geo.maxadv : HH_PF;
     c.G = geo.G;
 
     // The next tile's words are loaded one tile ahead into registers and
@@ -349,6 +366,10 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
     auto clampt = [&](uint64_t tt) { return tt < tlast ? tt : tlast; };
     Prefetch pf;
     uint64_t t = (uint64_t)blockIdx.x * HH_FW + wv;
+    // deferred walks: this wave's list q[qbase, qbase + qn), its length -> qn[gw]
+    const uint32_t gw = (uint32_t)t;
+    const uint64_t qbase = (uint64_t)gw * geo.qcap;
+    uint32_t qn = 0;
     if (t < geo.ntiles) {
         prefetch_wtile<SW>(pf, gdata, t * tile_bits / 32, geo.nwords);
         store_wtile<SW>(pf, s_w);
@@ -363,32 +384,41 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
         DIAG_STAMP(0);
 
         // pass 1: the head (from G bits before the region, lanes > 0), then
-        // the own chain from its entry point y, counted and masked
+        // the own chain from its entry point y, counted
         const uint32_t p0 = j * S;
-        uint32_t n = 0, x = bt;
-        uint64_t head = 0;
+        uint32_t n = 0, x = bt, y = bt;
         if (p0 < bt) {
-            const uint32_t y = j > 0 && c.G ? hh_region_head(&c, p0 - c.G, p0, &head) : p0;
+            y = j > 0 && c.G ? hh_region_head(&c, p0 - c.G, p0, nullptr) : p0;
             const uint32_t lim = p0 + S < bt ? p0 + S : bt;
-            x = y < lim ? hh_region_count(&c, y, lim, &n, s_mk) : y;
+            x = y < lim ? hh_region_count(&c, y, lim, &n) : y;
         }
-        s_x[j] = x;
-        s_n[j] = (uint16_t)n;
-        WAVE_SYNC();
+        s_y[j] = y;
         DIAG_STAMP(1);
-        // region j+1's chain met this one in the overlap window: merged at
-        // this chain's exit, no walk.  Its head comes from the next lane; the
-        // last lane walks into the next tile (two pointers).
+        // chain j's exit is chain j+1's entry point: merged there, no walk
+        // (the next tile's region 0 is entered at its start)
         const uint32_t R1 = (j + 1) * S;
-        const uint32_t hlo = (uint32_t)__shfl_down((int)(uint32_t)head, 1, 64);
-        const uint32_t hhi = (uint32_t)__shfl_down((int)(uint32_t)(head >> 32), 1, 64);
-        const bool merged = c.G && j != 63u && R1 < bt &&
-                            hh_window_merge(&c, s_mk, ((uint64_t)hhi << 32) | hlo, R1);
+        const uint32_t yn = (uint32_t)__shfl_down((int)y, 1, 64);
+        const bool merged = R1 < bt && x == (j == 63u ? R1 : yn);
+        WAVE_SYNC();                                    // s_y complete
 
-        // walks: region j's exit against the next regions' own chains
+        // walks: region j's exit against the next regions' own chains, two
+        // pointers, at most geo.fwalk lookups here
         hh_wk w = {1u, x - R1, 0u, 0, 0u, 0u};
-        if (!merged) w = hh_walk(&c, j, S, x, s_mk, s_x, s_n, HH_NR);
-        if (w.k == 0) {
+        if (!merged) w = hh_walk(&c, j, S, x, nullptr, nullptr, nullptr, 0, geo.fwalk, s_y, HH_NR);
+        uint32_t rec = rec_pack(w.k ? w.k : 1u, w.e, w.delta, n + w.cov);
+        if (w.more) {
+            rec = x | (n << 16);                        // k_walk's input: the exit and the count
+            const uint64_t dm = __ballot(1);            // (the deferring lanes)
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
+            wk.q[qbase + qn + rank] = (uint32_t)(t * HH_NR + j);
+        }
+        {
+            // the wave's own list (an atomic on one counter per deferring
+            // wave serialises: 4 ms per decode)
+            const uint64_t dm = __ballot(w.more);
+            qn += (uint32_t)__builtin_popcountll(dm);
+        }
+        if (!w.more && w.k == 0) {
             atomicOr(wk.flags, (uint32_t)F_FAIL);
             if (atomicCAS(&wk.flags[4], 0u, 1u) == 0u) {
                 wk.flags[5] = (uint32_t)t; wk.flags[6] = j; wk.flags[7] = x; wk.flags[8] = n; wk.flags[9] = bt;
@@ -411,20 +441,124 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
         }
 #endif
         DIAG_STAMP(2);
-        const uint32_t kk = w.k ? w.k : 1u;
-        const uint32_t mem = resolve_live_wave(kk, s_ka[wv], s_mema[wv]);
         // the walks are done: the next tile's words go to LDS now, and the
         // tile after it is loaded
         WAVE_SYNC();
         store_wtile<SW>(pf, s_w);
         prefetch_wtile<SW>(pf, gdata, clampt(t + 2 * nwv) * tile_bits / 32, geo.nwords);
+        wk.recs[t * HH_NR + j] = rec;
+        DIAG_STAMP(3);
+    }
+    if (j == 0) wk.qn[gw] = qn;
+    DIAG_FLUSH(dbg);
+}
 
-        // transfer table: charged count and leaving state for every entering d
-        const int32_t charged = (int32_t)(n + w.cov) + w.delta;
+// ---------------------------------------------------------------------------
+// k_walk: the deferred walks (k_front's queue), one lane each, over the
+// lane's own staging of the words it can reach: from G bits before region
+// j+1 to HH_KM regions further and a halo, at LDS index (g - g0) * 64 + lane
+// (a wave's lanes in distinct banks).  Two pointers from the exit, as in
+// k_front; the lane's record replaces k_front's (exit, count).
+// ---------------------------------------------------------------------------
+template <uint32_t SW>
+struct WalkWin {
+    static constexpr uint32_t n = (2 + HH_KM * SW + 4 + 3 + 3) & ~3u;   // words (x4 loads from g0 & ~3)
+};
+
+template <uint32_t SW>
+__global__ __launch_bounds__(64) void k_walk(const uint32_t *__restrict__ gdata, Geometry geo, DevTab tab, Work wk) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr uint32_t S = 32 * SW, NWIN = WalkWin<SW>::n;
+    const uint32_t lane = threadIdx.x;
+    uint16_t *s_f = (uint16_t *)smem;                   // F, its escape directory, L2
+    uint32_t *s_fdir = (uint32_t *)smem + HH_F_SIZE / 2;
+    uint32_t *s_l2 = s_fdir + ((tab.fdir_used + 3u) & ~3u);
+    uint32_t *s_win = (uint32_t *)smem + ftab_words(tab.fdir_used, tab.l2_used);   // NWIN x 64 words
+    load_ftables(tab, s_f, s_fdir, s_l2);
+    __syncthreads();
+    const uint64_t tile_bits = (uint64_t)HH_NR * S;
+    const uint32_t span = HH_NCOL * S;
+    hh_ctx c;
+    c.sw = 1024;                                        // hh_idx(g) = g * 64: one column per lane
+    c.nls = 64;
+    c.magic = 0;
+    c.l1m = nullptr;
+    c.l1s = nullptr;
+    c.l1 = nullptr;
+    c.f = s_f;
+    c.fdir = s_fdir;
+    c.pf = HH_PF;
+    c.l2 = s_l2;
+    c.tree = tab.tree;
+    c.tsym = tab.tsym;
+    c.maxadv = geo.maxadv > HH_PF ? geo.maxadv : HH_PF;
+    c.G = geo.G;
+    // one k_front wave's list at a time, its entries over the lanes
+    uint32_t fw = blockIdx.x, i = lane, cnt = fw < geo.nfw ? wk.qn[fw] : 0u;
+    for (;;) {
+        while (i >= cnt && fw < geo.nfw) {
+            i -= cnt;
+            fw += gridDim.x;
+            cnt = fw < geo.nfw ? wk.qn[fw] : 0u;
+        }
+        if (fw >= geo.nfw) break;
+        const uint32_t gl = wk.q[(uint64_t)fw * geo.qcap + i];
+        i += 64;
+        const uint64_t t = gl / HH_NR;
+        const uint32_t j = gl % HH_NR;
+        const uint32_t r0 = wk.recs[gl];
+        const uint32_t x = r0 & 0xffffu, n = r0 >> 16;
+        const uint64_t rem = geo.bits - t * tile_bits;
+        c.bt = rem < span ? (uint32_t)rem : span;
+        const uint32_t g0 = ((j + 1) * SW >= 2 ? (j + 1) * SW - 2 : 0u) & ~3u;
+        const __amdgpu_buffer_rsrc_t r = words_rsrc(gdata, t * tile_bits / 32, geo.nwords);
+#pragma unroll
+        for (uint32_t q = 0; q < NWIN; q += 4) {
+            const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(4u * (g0 + q)), 0, 0));
+            s_win[(q + 0) * 64 + lane] = v.x;
+            s_win[(q + 1) * 64 + lane] = v.y;
+            s_win[(q + 2) * 64 + lane] = v.z;
+            s_win[(q + 3) * 64 + lane] = v.w;
+        }
+        c.w = s_win + lane - g0 * 64;                   // (tile word g at (g - g0) * 64 + lane)
+        const hh_wk w = hh_walk(&c, j, S, x);
+        if (w.k == 0) {
+            atomicOr(wk.flags, (uint32_t)F_FAIL);
+            if (atomicCAS(&wk.flags[4], 0u, 1u) == 0u) {
+                wk.flags[5] = (uint32_t)t; wk.flags[6] = j; wk.flags[7] = x; wk.flags[8] = n; wk.flags[9] = c.bt;
+            }
+        } else {
+            wk.recs[gl] = rec_pack(w.k, w.e, w.delta, n + w.cov);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_table: the transfer table of every tile from its lane records, one tile
+// per wave: live masks over the entering state d < HH_KM, the charged count
+// of the live lanes and the state leaving the tile (from the last live lane,
+// the one whose walk crosses the tile end); CONST when the leaving state
+// does not depend on d.
+// ---------------------------------------------------------------------------
+#define HH_TABLE_W 4
+__global__ __launch_bounds__(64 * HH_TABLE_W) void k_table(Geometry geo, Work wk) {
+    __shared__ uint8_t s_ka[HH_TABLE_W][HH_NR];
+    __shared__ uint8_t s_mema[HH_TABLE_W][HH_NR];
+    __shared__ int32_t s_cda[HH_TABLE_W][HH_KM];
+    __shared__ uint32_t s_osta[HH_TABLE_W][HH_KM];
+    const uint32_t j = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    int32_t *s_cd = s_cda[wv];
+    uint32_t *s_ost = s_osta[wv];
+    for (uint64_t t = (uint64_t)blockIdx.x * HH_TABLE_W + wv; t < geo.ntiles; t += (uint64_t)gridDim.x * HH_TABLE_W) {
+        const uint32_t rec = wk.recs[t * HH_NR + j];
+        const uint32_t kk = rec_k(rec), e = rec_e(rec);
+        const int32_t delta = rec_delta(rec);
+        const uint32_t mem = resolve_live_wave(kk, s_ka[wv], s_mema[wv]);
+        const int32_t charged = (int32_t)rec_nc(rec) + delta;
         if (j < HH_KM) s_cd[j] = 0;
         WAVE_SYNC();
         if (j + kk >= HH_NR) {
-            const uint32_t os = hh_state_pack(j + kk - HH_NR, w.e, w.delta);
+            const uint32_t os = hh_state_pack(j + kk - HH_NR, e, delta);
 #pragma unroll
             for (uint32_t d = 0; d < HH_KM; d++)
                 if ((mem >> d) & 1u) s_ost[d] = os;
@@ -439,19 +573,14 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
                 if ((mem >> d) & 1u) atomicAdd(&s_cd[d], charged);
         }
         WAVE_SYNC();
-        wk.recs[t * HH_NR + j] = rec_pack(kk, w.e, w.delta, n + w.cov);
-        {
-            const uint32_t dd = j < HH_KM ? j : 0u;
-            const int32_t cnt = s_cd[dd] + v;
-            const uint32_t os = s_ost[dd];
-            // CONST: the leaving state is the same for every entering d
-            const bool cst = __ballot(j < HH_KM && os != s_ost[0]) == 0;
-            if (j < HH_KM)
-                wk.tabs[t * HH_KM + j] = hh_tab_pack(cnt, os) | (j == 0 && cst ? HH_CST : 0ull);
-        }
-        DIAG_STAMP(3);
+        const uint32_t dd = j < HH_KM ? j : 0u;
+        const int32_t cnt = s_cd[dd] + v;
+        const uint32_t os = s_ost[dd];
+        // CONST: the leaving state is the same for every entering d
+        const bool cst = __ballot(j < HH_KM && os != s_ost[0]) == 0;
+        if (j < HH_KM) wk.tabs[t * HH_KM + j] = hh_tab_pack(cnt, os) | (j == 0 && cst ? HH_CST : 0ull);
+        WAVE_SYNC();                                    // s_cd / s_ost read before the next tile
     }
-    DIAG_FLUSH(dbg);
 }
 
 // ---------------------------------------------------------------------------
@@ -976,6 +1105,8 @@ struct hh_decoder {
     hh_tables *ht;
     int have_tree;
     uint64_t *d_l1;
+    uint16_t *d_f;
+    uint32_t *d_fdir;
     uint32_t *d_l2;
     uint32_t *d_tree;
     uint8_t *d_tsym;
@@ -990,10 +1121,12 @@ struct hh_decoder {
     uint64_t *d_dbg;     // HH_DIAG counters (16 x u64)
     hipEvent_t ev[4];
     hh_stats stats;
-    uint32_t grid_f, grid_e;   // persistent grid sizes (occupancy x CUs)
+    uint32_t grid_f, grid_e, grid_w;   // persistent grid sizes (occupancy x CUs)
+    uint32_t fwalk;            // k_front's walk bound (HH_FRONT_WALK overrides)
     uint32_t grid_sw;          // words per region they were sized for
     size_t grid_l2;            // and the L2 table size
     uint32_t grid_tree;        // and the LDS tree size
+    uint32_t grid_fdir;        // and the F escape directory
     // host staging of the evaluate() scope (hh_decode_host)
     uint8_t *h_stage;          // 2 x HH_HOST_CHUNK pinned (hh_decode_host)
     hipEvent_t h_ev[2];
@@ -1030,6 +1163,8 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&d->d_l1, sizeof(uint64_t) * HH_L1_SIZE) != hipSuccess ||
         hipMalloc(&d->d_l2, sizeof(uint32_t) * HH_L2_MAX) != hipSuccess ||
+        hipMalloc(&d->d_f, sizeof(uint16_t) * HH_F_SIZE) != hipSuccess ||
+        hipMalloc(&d->d_fdir, sizeof(uint32_t) * HH_L2_MAX) != hipSuccess ||
         hipMalloc(&d->d_tree, sizeof(uint32_t) * (HH_TREE_MAX + 1)) != hipSuccess ||
         hipMalloc(&d->d_tsym, HH_TREE_MAX + 1) != hipSuccess ||
         hipMalloc(&d->d_max, 16) != hipSuccess ||
@@ -1054,6 +1189,8 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
     if (d->ws) hipFree(d->ws);
     if (d->d_l1) hipFree(d->d_l1);
     if (d->d_l2) hipFree(d->d_l2);
+    if (d->d_f) hipFree(d->d_f);
+    if (d->d_fdir) hipFree(d->d_fdir);
     if (d->d_tree) hipFree(d->d_tree);
     if (d->d_tsym) hipFree(d->d_tsym);
     if (d->d_max) hipFree(d->d_max);
@@ -1103,6 +1240,11 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     HIP_OK(hipMemcpy(d->d_l2, d->ht->l2, sizeof(uint32_t) * HH_L2_MAX, hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d->d_tree, d->ht->tree, sizeof(uint32_t) * (HH_TREE_MAX + 1), hipMemcpyHostToDevice));
     HIP_OK(hipMemcpy(d->d_tsym, d->ht->tsym, HH_TREE_MAX + 1, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d->d_f, d->ht->f, sizeof(d->ht->f), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d->d_fdir, d->ht->fdir, sizeof(uint32_t) * (d->ht->fdir_used ? d->ht->fdir_used : 1), hipMemcpyHostToDevice));
+    d->tab.f = d->d_f;
+    d->tab.fdir = d->d_fdir;
+    d->tab.fdir_used = d->ht->fdir_used;
     d->tab.l1 = d->d_l1;
     d->tab.l2 = d->d_l2;
     d->tab.tree = d->d_tree;
@@ -1110,6 +1252,9 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     d->tab.l2_used = d->ht->l2_used;
     d->tab.tree_lds = d->ht->tree_used;
     d->S = pick_region_bits(d->ht, d->cfg.lane_bits);
+    d->fwalk = HH_FRONT_WALK;
+    const char *fw = getenv("HH_FRONT_WALK");            // experiments
+    if (fw && *fw) d->fwalk = (uint32_t)atoi(fw);
     d->G = hh_pick_overlap(d->ht);
     if (getenv("HH_OVERLAP")) d->G = (uint32_t)atoi(getenv("HH_OVERLAP")) & ~31u;   // experiments
     if (d->G > HH_GMAX || d->G + 32 > d->S) d->G = 0;
@@ -1138,8 +1283,12 @@ static int fast_path_ok(const hh_decoder *d) {
 static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8_t *d_out,
                           uint64_t cap, uint64_t *out_len, hipStream_t st);
 
-static size_t lds_front(uint32_t sw, uint32_t l2) {
-    return ((size_t)HH_L1_SIZE + ((l2 + 3) & ~3u) + (size_t)HH_FW * 2 * sw * HH_NLS) * 4;
+static size_t lds_front(uint32_t sw, uint32_t l2, uint32_t fdir) {
+    return ((size_t)ftab_words(fdir, l2) + (size_t)HH_FW * sw * HH_NLS) * 4;
+}
+static uint32_t walk_win(uint32_t sw) { return (2 + HH_KM * sw + 4 + 3 + 3) & ~3u; }   // WalkWin<sw>::n
+static size_t lds_walk(uint32_t sw, uint32_t l2, uint32_t fdir) {
+    return ((size_t)ftab_words(fdir, l2) + (size_t)walk_win(sw) * 64) * 4;
 }
 static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree) {
     return (2 * (size_t)HH_L1_SIZE + (size_t)HH_NW * sw * HH_NLS + l2) * 4 + (size_t)HH_NW * HH_OBW +
@@ -1156,6 +1305,15 @@ static kfront_t kfront_for(uint32_t sw) {
     default: return nullptr;
     }
 }
+typedef void (*kwalk_t)(const uint32_t *, Geometry, DevTab, Work);
+static kwalk_t kwalk_for(uint32_t sw) {
+    switch (sw) {
+#define X(n) case n: return k_walk<n>;
+        HH_SW_CASES(X)
+#undef X
+    default: return nullptr;
+    }
+}
 static kemit_t kemit_for(uint32_t sw) {
     switch (sw) {
 #define X(n) case n: return k_emit<n>;
@@ -1167,18 +1325,22 @@ static kemit_t kemit_for(uint32_t sw) {
 
 // Persistent grids: the occupancy answer x CUs for each kernel.
 static int size_grids(hh_decoder *d, uint32_t sw) {
-    if (d->grid_f && d->grid_sw == sw && d->grid_l2 == d->tab.l2_used && d->grid_tree == d->tab.tree_lds)
+    if (d->grid_f && d->grid_sw == sw && d->grid_l2 == d->tab.l2_used && d->grid_tree == d->tab.tree_lds &&
+        d->grid_fdir == d->tab.fdir_used)
         return HH_OK;
-    int pf = 0, pe = 0, ncu = 0;
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pf, kfront_for(sw), 64 * HH_FW, lds_front(sw, d->tab.l2_used)));
+    int pf = 0, pe = 0, pw = 0, ncu = 0;
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pf, kfront_for(sw), 64 * HH_FW, lds_front(sw, d->tab.l2_used, d->tab.fdir_used)));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, kwalk_for(sw), 64, lds_walk(sw, d->tab.l2_used, d->tab.fdir_used)));
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kemit_for(sw), HH_NL, lds_emit(sw, d->tab.l2_used, d->tab.tree_lds)));
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
-    if (pf < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
+    if (pf < 1 || pe < 1 || pw < 1) return HH_ERR_UNSUPPORTED;
     d->grid_f = (uint32_t)(pf * ncu);
+    d->grid_w = (uint32_t)(pw * ncu);
     d->grid_e = (uint32_t)(pe * ncu);
     d->grid_sw = sw;
     d->grid_l2 = d->tab.l2_used;
     d->grid_tree = d->tab.tree_lds;
+    d->grid_fdir = d->tab.fdir_used;
     return HH_OK;
 }
 
@@ -1252,17 +1414,26 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     geo.nwords = ((bits_avail + 7) / 8 + HH_PAYLOAD_PAD) / 4;
     geo.in_state = in_state;
     geo.emit_from = emit_from;
+    geo.fwalk = d->fwalk;
     const uint64_t tb = (uint64_t)HH_NR * d->S;
     const uint64_t all = (bits_avail + tb - 1) / tb;
     geo.ntiles = ntiles && ntiles < all ? ntiles : all;
     geo.vec4 = (((uintptr_t)d_data & 15u) == 0) && (geo.sw % 4 == 0);
     const uint64_t nt = geo.ntiles;
     const uint32_t nblk = (uint32_t)((nt + 1 + HH_SCAN_TB - 1) / HH_SCAN_TB);
-    // workspace: flags 64 B | tabs | recs | st | lex | blk
+    // workspace: flags 64 B | tabs | recs | st | lex | blk | q
     const size_t o_tabs = 64, o_recs = o_tabs + nt * HH_KM * 8, o_st = o_recs + nt * HH_NR * 4;
     const size_t o_lex = (o_st + (nt + 1) * 4 + 7) & ~(size_t)7, o_blk = (o_lex + (nt + 1) * 4 + 7) & ~(size_t)7;
-    const size_t need = o_blk + (size_t)nblk * 8;
-    int rc = ensure_dev(&d->ws, &d->ws_size, need);
+    int rc = size_grids(d, geo.sw);
+    if (rc) return rc;
+    // one tile per wave at a time in both kernels
+    const uint64_t nfw = (nt + HH_FW - 1) / HH_FW;
+    const uint32_t gf = (uint32_t)(nfw < d->grid_f ? nfw : d->grid_f);
+    geo.nfw = gf * HH_FW;
+    geo.qcap = (nt + geo.nfw - 1) / geo.nfw * HH_NR;
+    const size_t o_qn = o_blk + (size_t)nblk * 8, o_q = o_qn + (size_t)geo.nfw * 4;
+    const size_t need = o_q + (size_t)geo.nfw * geo.qcap * 4;
+    rc = ensure_dev(&d->ws, &d->ws_size, need);
     if (rc) return rc;
     uint8_t *w = (uint8_t *)d->ws;
     Work wk;
@@ -1272,14 +1443,12 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     wk.st = (uint32_t *)(w + o_st);
     wk.lex = (int32_t *)(w + o_lex);
     wk.blk = (int64_t *)(w + o_blk);
+    wk.q = (uint32_t *)(w + o_q);
+    wk.qn = (uint32_t *)(w + o_qn);
     const kfront_t kf = kfront_for(geo.sw);
+    const kwalk_t kw = kwalk_for(geo.sw);
     const kemit_t ke = kemit_for(geo.sw);
-    if (!kf || !ke) return HH_ERR_UNSUPPORTED;
-    rc = size_grids(d, geo.sw);
-    if (rc) return rc;
-    // one tile per wave at a time in both kernels
-    const uint64_t nfw = (nt + HH_FW - 1) / HH_FW;
-    const uint32_t gf = (uint32_t)(nfw < d->grid_f ? nfw : d->grid_f);
+    if (!kf || !kw || !ke) return HH_ERR_UNSUPPORTED;
     const uint64_t ne = nt > emit_from ? nt - emit_from : 0;
     const uint64_t ng = (ne + HH_NW - 1) / HH_NW;          // workgroups' worth of tiles
     const uint32_t ge = (uint32_t)(ng < d->grid_e ? (ng ? ng : 1) : d->grid_e);
@@ -1289,9 +1458,19 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     HIP_OK(hipMemsetAsync(d->d_dbg, 0, 16 * sizeof(uint64_t), st));
 #endif
     HIP_OK(hipEventRecord(d->ev[0], st));
-    hipLaunchKernelGGL(kf, dim3(gf), dim3(64 * HH_FW), lds_front(geo.sw, d->tab.l2_used), st,
+    hipLaunchKernelGGL(kf, dim3(gf), dim3(64 * HH_FW), lds_front(geo.sw, d->tab.l2_used, d->tab.fdir_used), st,
                        (const uint32_t *)d_data, geo, d->tab, wk, d->d_dbg);
     HIP_OK(hipGetLastError());
+    // the deferred walks (their count is on the device: a persistent grid)
+    hipLaunchKernelGGL(kw, dim3(d->grid_w), dim3(64), lds_walk(geo.sw, d->tab.l2_used, d->tab.fdir_used), st,
+                       (const uint32_t *)d_data, geo, d->tab, wk);
+    HIP_OK(hipGetLastError());
+    {
+        const uint64_t nb = (nt + HH_TABLE_W - 1) / HH_TABLE_W;
+        hipLaunchKernelGGL(k_table, dim3((unsigned)(nb < (1u << 20) ? nb : (1u << 20))), dim3(64 * HH_TABLE_W), 0, st,
+                           geo, wk);
+        HIP_OK(hipGetLastError());
+    }
     HIP_OK(hipEventRecord(d->ev[1], st));
     hipLaunchKernelGGL(k_scan1, dim3(nblk), dim3(HH_SCAN_TB), 0, st, geo, wk);
     HIP_OK(hipGetLastError());

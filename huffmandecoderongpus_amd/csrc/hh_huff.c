@@ -389,5 +389,37 @@ int hh_tables_build(const void *tree_v, hh_tables *T) {
         }
         T->l1[w] = e;
     }
+
+    /* F (the front kernel's table): every complete symbol of HH_PF bits */
+    int16_t slot[HH_L1_SIZE];
+    for (uint32_t i = 0; i < HH_L1_SIZE; i++) slot[i] = -1;
+    for (uint32_t w = 0; w < HH_F_SIZE; w++) {
+        uint32_t node = 0, nbits = 0, bm = 0;
+        unsigned pos = 0, start = 0;
+        while (pos < HH_PF) {
+            node = tchild(T, node, (w >> pos) & 1);
+            pos++;
+            if (tleaf(T, node)) {
+                bm |= 1u << start;
+                nbits = pos;
+                node = 0;
+                start = pos;
+            }
+        }
+        if (nbits) {
+            T->f[w] = (uint16_t)(nbits | ((bm >> 1) << 4));
+        } else {
+            /* first code longer than HH_PF (>= HH_P) bits: its first HH_P
+             * bits index an L1 escape entry; F points at a copy of its
+             * meta half */
+            const uint32_t i1 = w & (HH_L1_SIZE - 1u);
+            if (slot[i1] < 0) {
+                if (T->fdir_used >= HH_L2_MAX) return HH_ERR_UNSUPPORTED;
+                slot[i1] = (int16_t)T->fdir_used;
+                T->fdir[T->fdir_used++] = (uint32_t)(T->l1[i1] >> 32);
+            }
+            T->f[w] = (uint16_t)((uint32_t)slot[i1] << 4);
+        }
+    }
     return HH_OK;
 }

@@ -29,6 +29,16 @@
  *     no leaf:  bits 0..23 compact node id at depth HH_P+q (continue with a
  *               bit-serial walk -- only for codes longer than HH_P+HH_Q_MAX)
  *
+ *   F[2^HH_PF]  u16, the front kernel's table (it needs no symbol bytes):
+ *               indexed by the next HH_PF stream bits like L1, every complete
+ *               symbol in the window (no HH_K cap)
+ *     bits  0..3   nbits of those symbols (0 = escape: first code longer
+ *                  than HH_PF bits)
+ *     bits  4..15  start offsets 1..12 of the symbols after the first
+ *                  (bit i <=> a symbol starts at offset i + 1)
+ *     escape:      bits 4..15 index FDIR[], the meta half of the L1 escape
+ *                  entry of the first HH_P bits (its L2 subtable)
+ *
  *   tree[]      compact tree for walks (tail symbols, very long codes):
  *               u32 per compact node: bit 31 leaf; leaf -> bits 0..7 sym;
  *               internal -> bits 0..14 child0, bits 15..29 child1; internal
@@ -45,6 +55,10 @@
 #define HH_P 11                 /* L1 index bits                      */
 #endif
 #define HH_L1_SIZE (1u << HH_P)
+#ifndef HH_PF
+#define HH_PF 12                /* F index bits (11 <= HH_PF <= 13)    */
+#endif
+#define HH_F_SIZE (1u << HH_PF)
 #define HH_Q_MAX 9              /* max L2 subtable index bits         */
 #define HH_L2_MAX 4096          /* L2 entries kept (LDS budget 16 KB) */
 #define HH_TREE_MAX 32767       /* compact nodes (15-bit ids)         */
@@ -65,6 +79,9 @@ typedef struct {
     uint64_t l1[HH_L1_SIZE];
     uint32_t l2[HH_L2_MAX];
     uint32_t l2_used;
+    uint16_t f[HH_F_SIZE];
+    uint32_t fdir[HH_L2_MAX];
+    uint32_t fdir_used;
     uint32_t tree[HH_TREE_MAX + 1];
     uint8_t tsym[HH_TREE_MAX + 1];
     uint32_t tree_used;

@@ -61,7 +61,12 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
     const uint64_t nbytes = (bits + 7) / 8;
     const uint32_t span = HH_NCOL * S;
     std::vector<uint32_t> w((size_t)sw * HH_NLS);
-    std::vector<uint32_t> xs(HH_NR), ns(HH_NR), mem(HH_NR), ent(HH_NR);
+    std::vector<uint32_t> xs(HH_NR), ys(HH_NR), ns(HH_NR), mem(HH_NR), ent(HH_NR);
+    // k_walk's staging of a deferred walk: words g0 .. g0 + nwin of the tile
+    // at LDS index (g - g0) * 64 + lane (emulated for lane 0)
+    const uint32_t fw = getenv("HH_FRONT_WALK") ? (uint32_t)atoi(getenv("HH_FRONT_WALK")) : HH_FRONT_WALK;
+    std::vector<uint32_t> win((size_t)(HH_NCOL * HH_SW_MAX + 8) * 64);
+    int64_t ndefer = 0;
     std::vector<uint16_t> n16(HH_NR);
     std::vector<uint32_t> l1m(HH_L1_SIZE), l1s(HH_L1_SIZE);   // split L1, as staged in LDS
     for (uint32_t i = 0; i < HH_L1_SIZE; i++) {
@@ -73,6 +78,9 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
     std::vector<int32_t> din(HH_NR);
     std::vector<hh_wk> wk(HH_NR);
     stats[0] = (int64_t)ntiles;
+    // HH_EMU_HIST: walk-length statistics (lookups per lane, longest per tile)
+    const bool hist = getenv("HH_EMU_HIST") != nullptr;
+    std::vector<uint64_t> hl(1025, 0), ht(1025, 0);
 
     auto word_at = [&](uint64_t gw) -> uint32_t {
         uint32_t v = 0;
@@ -108,6 +116,12 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
         const uint64_t rem = bits - t * TB;
         c.bt = rem < span ? (uint32_t)rem : span;
         const uint32_t bt = c.bt;
+        // the front kernels' context: lookups through F (no symbol bytes)
+        hh_ctx cf = c;
+        cf.f = T.f;
+        cf.fdir = T.fdir;
+        cf.pf = HH_PF;
+        if (cf.maxadv < HH_PF) cf.maxadv = HH_PF;
 
         for (size_t i = 0; i < mk.size(); i++)          // words pass 1 leaves unwritten
             mk[i] = (uint32_t)(0x9e3779b9u * (uint32_t)(i + t * 7919u + 1));   // hold junk
@@ -115,26 +129,63 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
             uint32_t p0 = j * S, n = 0, x = bt, y = p0;
             hd[j] = 0;
             if (p0 < bt) {
-                if (j > 0 && G) y = hh_region_head(&c, p0 - G, p0, &hd[j]);
+                if (j > 0 && G) y = hh_region_head(&cf, p0 - G, p0, &hd[j]);
                 uint32_t lim = p0 + S < bt ? p0 + S : bt;
-                x = y < lim ? hh_region_count(&c, y, lim, &n, mk.data()) : y;
+                x = y < lim ? hh_region_count(&cf, y, lim, &n, mk.data()) : y;
             }
             xs[j] = x;
+            ys[j] = p0 < bt ? y : bt;
             ns[j] = n;
             n16[j] = (uint16_t)n;
         }
-        for (uint32_t j = 0; j < HH_NR; j++) {            // window checks, else walks
+        for (uint32_t j = 0; j < HH_NR; j++) {            // merges at the exit, else walks
             const uint32_t R1 = (j + 1) * S;
-            if (G && j + 1 < HH_NR && R1 < bt && hh_window_merge(&c, mk.data(), hd[j + 1], R1)) {
-                wk[j] = hh_wk{1u, xs[j] - R1, 0u, 0, 0u, 0u};
+            // the kernel's rule: chain j's exit is chain j+1's entry point
+            const uint32_t ynext = j + 1 < HH_NR ? ys[j + 1] : R1;
+            const bool merged = R1 < bt && xs[j] == ynext;
+            // the round-1 rule it replaces (boundary masks in the overlap window)
+            const bool wmerged = G && j + 1 < HH_NR && R1 < bt && hh_window_merge(&c, mk.data(), hd[j + 1], R1);
+            if (wmerged && !merged) return HH_ERR_INTERNAL - 501;
+            // reference result: the mask walk over the whole tile
+            const hh_wk ref = merged ? hh_wk{1u, xs[j] - R1, 0u, 0, 0u, 0u}
+                                     : hh_walk(&c, j, S, xs[j], mk.data(), xs.data(), n16.data(), HH_NR);
+            if (merged) {
+                wk[j] = ref;
                 continue;
             }
-            wk[j] = hh_walk(&c, j, S, xs[j], mk.data(), xs.data(), n16.data(), HH_NR);
+            // the kernel's: a two-pointer walk of at most fw lookups in k_front,
+            // else again from the exit in k_walk over its own staging
+            wk[j] = hh_walk(&cf, j, S, xs[j], nullptr, nullptr, nullptr, 0, fw, ys.data(), HH_NR);
+            if (wk[j].more) {
+                ndefer++;
+                const uint32_t g0 = (j + 1) * sw >= 2 ? (j + 1) * sw - 2 : 0;
+                const uint32_t nwin = 2 + HH_KM * sw + 4;
+                for (uint32_t q = 0; q < nwin; q++) win[(size_t)(g0 + q) * 64] = word_at(tw0 + g0 + q);
+                hh_ctx cw = cf;
+                cw.w = win.data();
+                cw.sw = 1024;
+                cw.nls = 64;
+                wk[j] = hh_walk(&cw, j, S, xs[j]);
+            }
+            if (wk[j].k != ref.k || (ref.k && (wk[j].e != ref.e || wk[j].cov != ref.cov || wk[j].delta != ref.delta))) {
+                fprintf(stderr, "emu: tile %lu lane %u walk (k %u e %u cov %u delta %d) vs mask walk (k %u e %u cov %u delta %d)\n",
+                        (unsigned long)t, j, wk[j].k, wk[j].e, wk[j].cov, wk[j].delta, ref.k, ref.e, ref.cov, ref.delta);
+                return HH_ERR_INTERNAL - 500;
+            }
             if (wk[j].k == 0) stats[2]++;
             if (wk[j].k > 1) stats[1]++;
             if ((int64_t)wk[j].k > stats[4]) stats[4] = wk[j].k;
         }
         if (stats[2]) return HH_ERR_UNSUPPORTED;
+        if (hist) {
+            uint32_t mx = 0;
+            for (uint32_t j = 0; j < HH_NR; j++) {
+                const uint32_t s = wk[j].steps < 1024 ? wk[j].steps : 1024;
+                hl[s]++;
+                mx = s > mx ? s : mx;
+            }
+            ht[mx]++;
+        }
         // transfer table
         for (uint32_t j = 0; j < HH_NR; j++) mem[j] = hh_mem_init(j);
         for (uint32_t j = 0; j < HH_NR; j++)              // exceptions, ascending
@@ -221,6 +272,11 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
         st_in = so;
     }
     if (leave) *leave = st_in;
+    if (hist) {
+        fprintf(stderr, "deferred %ld of %lu lanes\n", (long)ndefer, (unsigned long)(ntiles * HH_NR));
+        for (uint32_t b = 0; b <= 1024; b++)
+            if (hl[b] || ht[b]) fprintf(stderr, "hist %u lanes %lu tiles %lu\n", b, (unsigned long)hl[b], (unsigned long)ht[b]);
+    }
     return (int64_t)base;
 }
 
