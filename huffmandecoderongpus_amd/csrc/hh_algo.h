@@ -74,7 +74,7 @@
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
                                  as a failed walk) */
 #ifndef HH_FRONT_WALK
-#define HH_FRONT_WALK 16      /* lookups of a walk in k_front; longer walks are
+#define HH_FRONT_WALK 4       /* lookups of a walk in k_front; longer walks are
                                  deferred to k_walk (a wave would wait for its
                                  longest walk) */
 #endif
@@ -559,6 +559,38 @@ HH_HD hh_wk hh_walk(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x,
     r.more = it >= maxit && maxit < HH_WALK_MAX;
     r.steps = it;
     return r;   /* k == 0: failed (or, with more, not finished yet) */
+}
+
+/* The deferred walks (k_walk): the chain W leaving region j at x, followed
+ * region by region to its exit only.  W meets region r's own chain C_r iff
+ * their exits from r coincide (a shared boundary makes the chains identical
+ * from there on; equal exits are a shared boundary), and then W's symbols
+ * in r minus C_r's symbols in r equal their difference before the first
+ * shared boundary -- so the result is hh_walk's (k, e, cov, delta), given
+ * each region's pass-1 exit xr[k] and count nr[k] (k = 1..HH_KM: region
+ * j+k).  Every lookup is a cursor step (no second pointer, no heads). */
+HH_HD hh_wk hh_walk_exits(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x, const uint32_t *xr,
+                          const uint32_t *nr) {
+    hh_wk r = {0u, 0u, 0u, 0, 0u, 0u};
+    const uint32_t bt = c->bt;
+    uint32_t A = x < bt ? x : bt, ca = 0;
+    for (uint32_t k = 1; k <= HH_KM; k++) {
+        const uint32_t R = (j + k) * S;
+        const uint32_t Ec = R + S < bt ? R + S : bt;
+        const uint32_t e = A > R ? A - R : 0u;
+        uint32_t n = 0;
+        if (A < Ec) A = hh_region_count(c, A, Ec, &n);
+        const uint32_t xk = xr[k] < bt ? xr[k] : bt;
+        if (A == xk) {
+            r.k = k;
+            r.e = e;
+            r.cov = ca;
+            r.delta = (int32_t)n - (int32_t)nr[k];
+            return r;
+        }
+        ca += n;
+    }
+    return r;   /* k == 0: no merge within HH_KM regions */
 }
 
 /* ------------------------------------------------------------------ */

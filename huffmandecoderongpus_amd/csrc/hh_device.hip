@@ -123,6 +123,7 @@ struct Work {
     int64_t *blk;        // [nblk] scan block totals, then exclusive block bases
     uint32_t *q;         // [nfw][qcap] deferred walks of each k_front wave (tile * HH_NR + lane)
     uint32_t *qn;        // [nfw] their counts
+    uint32_t *xn;        // [ntiles * HH_NR] pass-1 exit | count << 16 of every region
 };
 
 // ---------------------------------------------------------------------------
@@ -405,9 +406,8 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
         // pointers, at most geo.fwalk lookups here
         hh_wk w = {1u, x - R1, 0u, 0, 0u, 0u};
         if (!merged) w = hh_walk(&c, j, S, x, nullptr, nullptr, nullptr, 0, geo.fwalk, s_y, HH_NR);
-        uint32_t rec = rec_pack(w.k ? w.k : 1u, w.e, w.delta, n + w.cov);
+        const uint32_t rec = rec_pack(w.k ? w.k : 1u, w.e, w.delta, n + w.cov);
         if (w.more) {
-            rec = x | (n << 16);                        // k_walk's input: the exit and the count
             const uint64_t dm = __ballot(1);            // (the deferring lanes)
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
             wk.q[qbase + qn + rank] = (uint32_t)(t * HH_NR + j);
@@ -446,7 +446,8 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
         WAVE_SYNC();
         store_wtile<SW>(pf, s_w);
         prefetch_wtile<SW>(pf, gdata, clampt(t + 2 * nwv) * tile_bits / 32, geo.nwords);
-        wk.recs[t * HH_NR + j] = rec;
+        wk.recs[t * HH_NR + j] = rec;                 // (a deferred lane's: k_walk's)
+        wk.xn[t * HH_NR + j] = x | (n << 16);         // the region's exit and count, for k_walk
         DIAG_STAMP(3);
     }
     if (j == 0) wk.qn[gw] = qn;
@@ -454,11 +455,12 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
 }
 
 // ---------------------------------------------------------------------------
-// k_walk: the deferred walks (k_front's queue), one lane each, over the
+// k_walk: the deferred walks (k_front's lists), one lane each, over the
 // lane's own staging of the words it can reach: from G bits before region
 // j+1 to HH_KM regions further and a halo, at LDS index (g - g0) * 64 + lane
-// (a wave's lanes in distinct banks).  Two pointers from the exit, as in
-// k_front; the lane's record replaces k_front's (exit, count).
+// (a wave's lanes in distinct banks).  Exit comparisons (hh_walk_exits)
+// against the regions' pass-1 exits and counts (xn); the lane's record
+// replaces k_front's placeholder.
 // ---------------------------------------------------------------------------
 template <uint32_t SW>
 struct WalkWin {
@@ -506,22 +508,47 @@ __global__ __launch_bounds__(64) void k_walk(const uint32_t *__restrict__ gdata,
         i += 64;
         const uint64_t t = gl / HH_NR;
         const uint32_t j = gl % HH_NR;
-        const uint32_t r0 = wk.recs[gl];
+        const uint32_t r0 = wk.xn[gl];
         const uint32_t x = r0 & 0xffffu, n = r0 >> 16;
         const uint64_t rem = geo.bits - t * tile_bits;
         c.bt = rem < span ? (uint32_t)rem : span;
-        const uint32_t g0 = ((j + 1) * SW >= 2 ? (j + 1) * SW - 2 : 0u) & ~3u;
-        const __amdgpu_buffer_rsrc_t r = words_rsrc(gdata, t * tile_bits / 32, geo.nwords);
+        // exits and counts of regions j+1 .. j+HH_KM (the next tile's in its
+        // frame, + the tile's bits; past the decoded tiles: computed below)
+        uint32_t xr[HH_KM + 1], nr[HH_KM + 1], nmiss = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < NWIN; q += 4) {
-            const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(4u * (g0 + q)), 0, 0));
-            s_win[(q + 0) * 64 + lane] = v.x;
-            s_win[(q + 1) * 64 + lane] = v.y;
-            s_win[(q + 2) * 64 + lane] = v.z;
-            s_win[(q + 3) * 64 + lane] = v.w;
+        for (uint32_t k = 1; k <= HH_KM; k++) {
+            const uint32_t rg = j + k;
+            const bool nxt = rg >= HH_NR;
+            const bool have = !nxt || t + 1 < geo.ntiles;
+            const uint32_t v = have ? wk.xn[gl + k] : 0u;
+            xr[k] = (v & 0xffffu) + (nxt ? HH_NR * S : 0u);
+            nr[k] = v >> 16;
+            nmiss |= have ? 0u : 1u << k;
+        }
+        const uint32_t g0 = ((j + 1) * SW >= 2 ? (j + 1) * SW - 2 : 0u) & ~3u;
+        // plain loads (a buffer resource per lane would be a waterfall loop:
+        // one lane at a time); words past the payload are read clamped to
+        // its last readable ones -- they lie past the end of the stream,
+        // which no decision depends on
+        const uint64_t gw0 = t * tile_bits / 32 + g0, glim = geo.nwords;
+#pragma unroll
+        for (uint32_t q = 0; q < NWIN; q++) {
+            const uint64_t gi = gw0 + q;
+            s_win[q * 64 + lane] = gdata[gi < glim ? gi : glim - 1];
         }
         c.w = s_win + lane - g0 * 64;                   // (tile word g at (g - g0) * 64 + lane)
-        const hh_wk w = hh_walk(&c, j, S, x);
+        while (nmiss) {                                 // regions of a tile not decoded (a
+            const uint32_t k = __builtin_ctz(nmiss);    // range's end): their own pass 1
+            nmiss &= nmiss - 1;
+            const uint32_t rg = j + k, R = rg * S, bt = c.bt;
+            uint32_t yy = R < bt ? R : bt, nn = 0, xx = yy;
+            if (R < bt && c.G && rg % HH_NR) yy = hh_region_head(&c, R - c.G, R, nullptr);
+            const uint32_t lim = R + S < bt ? R + S : bt;
+            if (yy < lim) xx = hh_region_count(&c, yy, lim, &nn);
+            xr[k] = xx;
+            nr[k] = nn;
+        }
+        const hh_wk w = hh_walk_exits(&c, j, S, x, xr, nr);
         if (w.k == 0) {
             atomicOr(wk.flags, (uint32_t)F_FAIL);
             if (atomicCAS(&wk.flags[4], 0u, 1u) == 0u) {
@@ -549,12 +576,30 @@ __global__ __launch_bounds__(64 * HH_TABLE_W) void k_table(Geometry geo, Work wk
     const uint32_t j = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     int32_t *s_cd = s_cda[wv];
     uint32_t *s_ost = s_osta[wv];
-    for (uint64_t t = (uint64_t)blockIdx.x * HH_TABLE_W + wv; t < geo.ntiles; t += (uint64_t)gridDim.x * HH_TABLE_W) {
-        const uint32_t rec = wk.recs[t * HH_NR + j];
+    const uint64_t step = (uint64_t)gridDim.x * HH_TABLE_W;
+    uint64_t t = (uint64_t)blockIdx.x * HH_TABLE_W + wv;
+    const uint64_t tlast = geo.ntiles - 1;
+    uint32_t rec_n = t < geo.ntiles ? wk.recs[t * HH_NR + j] : 0u;
+    for (; t < geo.ntiles; t += step) {
+        const uint32_t rec = rec_n;
+        const uint64_t tn = t + step < tlast ? t + step : tlast;   // the next tile's record, ahead
+        rec_n = wk.recs[tn * HH_NR + j];
         const uint32_t kk = rec_k(rec), e = rec_e(rec);
         const int32_t delta = rec_delta(rec);
-        const uint32_t mem = resolve_live_wave(kk, s_ka[wv], s_mema[wv]);
         const int32_t charged = (int32_t)rec_nc(rec) + delta;
+        if (__ballot(kk > 1) == 0) {
+            // no exceptions: lane j is live for entering d <= j (all d from
+            // lane HH_KM - 1 on), so row d counts the lanes >= d; the last
+            // lane leaves the tile for every d (CONST)
+            const int32_t incl = wave_incl_scan(charged);
+            const int32_t tot = __builtin_amdgcn_readlane(incl, 63);
+            const uint32_t os = hh_state_pack(kk - 1u, e, delta);          // (lane 63: j + kk - HH_NR)
+            const uint32_t os63 = (uint32_t)__builtin_amdgcn_readlane((int)os, 63);
+            if (j < HH_KM)
+                wk.tabs[t * HH_KM + j] = hh_tab_pack(tot - (incl - charged), os63) | (j == 0 ? HH_CST : 0ull);
+            continue;
+        }
+        const uint32_t mem = resolve_live_wave(kk, s_ka[wv], s_mema[wv]);
         if (j < HH_KM) s_cd[j] = 0;
         WAVE_SYNC();
         if (j + kk >= HH_NR) {
@@ -1123,6 +1168,7 @@ struct hh_decoder {
     hh_stats stats;
     uint32_t grid_f, grid_e, grid_w;   // persistent grid sizes (occupancy x CUs)
     uint32_t fwalk;            // k_front's walk bound (HH_FRONT_WALK overrides)
+    uint32_t ncu;              // compute units
     uint32_t grid_sw;          // words per region they were sized for
     size_t grid_l2;            // and the L2 table size
     uint32_t grid_tree;        // and the LDS tree size
@@ -1336,6 +1382,7 @@ static int size_grids(hh_decoder *d, uint32_t sw) {
     if (pf < 1 || pe < 1 || pw < 1) return HH_ERR_UNSUPPORTED;
     d->grid_f = (uint32_t)(pf * ncu);
     d->grid_w = (uint32_t)(pw * ncu);
+    d->ncu = (uint32_t)ncu;
     d->grid_e = (uint32_t)(pe * ncu);
     d->grid_sw = sw;
     d->grid_l2 = d->tab.l2_used;
@@ -1432,7 +1479,8 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     geo.nfw = gf * HH_FW;
     geo.qcap = (nt + geo.nfw - 1) / geo.nfw * HH_NR;
     const size_t o_qn = o_blk + (size_t)nblk * 8, o_q = o_qn + (size_t)geo.nfw * 4;
-    const size_t need = o_q + (size_t)geo.nfw * geo.qcap * 4;
+    const size_t o_xn = o_q + (size_t)geo.nfw * geo.qcap * 4;
+    const size_t need = o_xn + nt * HH_NR * 4;
     rc = ensure_dev(&d->ws, &d->ws_size, need);
     if (rc) return rc;
     uint8_t *w = (uint8_t *)d->ws;
@@ -1445,6 +1493,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     wk.blk = (int64_t *)(w + o_blk);
     wk.q = (uint32_t *)(w + o_q);
     wk.qn = (uint32_t *)(w + o_qn);
+    wk.xn = (uint32_t *)(w + o_xn);
     const kfront_t kf = kfront_for(geo.sw);
     const kwalk_t kw = kwalk_for(geo.sw);
     const kemit_t ke = kemit_for(geo.sw);
@@ -1466,9 +1515,9 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
                        (const uint32_t *)d_data, geo, d->tab, wk);
     HIP_OK(hipGetLastError());
     {
-        const uint64_t nb = (nt + HH_TABLE_W - 1) / HH_TABLE_W;
-        hipLaunchKernelGGL(k_table, dim3((unsigned)(nb < (1u << 20) ? nb : (1u << 20))), dim3(64 * HH_TABLE_W), 0, st,
-                           geo, wk);
+        // persistent: each wave's next record is loaded a tile ahead
+        const uint64_t nb = (nt + HH_TABLE_W - 1) / HH_TABLE_W, cap = (uint64_t)d->ncu * 8;
+        hipLaunchKernelGGL(k_table, dim3((unsigned)(nb < cap ? nb : cap)), dim3(64 * HH_TABLE_W), 0, st, geo, wk);
         HIP_OK(hipGetLastError());
     }
     HIP_OK(hipEventRecord(d->ev[1], st));

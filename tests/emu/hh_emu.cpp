@@ -156,8 +156,22 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
             // the kernel's: a two-pointer walk of at most fw lookups in k_front,
             // else again from the exit in k_walk over its own staging
             wk[j] = hh_walk(&cf, j, S, xs[j], nullptr, nullptr, nullptr, 0, fw, ys.data(), HH_NR);
-            if (wk[j].more) {
-                ndefer++;
+            {
+                // k_walk's form of every walk: exits and counts of the regions
+                // it may reach (pass 1 of this tile; regions of the next tile
+                // from their own heads), then exit comparisons over k_walk's
+                // staging of the lane's words
+                uint32_t xr[HH_KM + 1], nr[HH_KM + 1];
+                for (uint32_t k = 1; k <= HH_KM; k++) {
+                    const uint32_t rg = j + k, R = rg * S;
+                    if (rg < HH_NR) { xr[k] = xs[rg]; nr[k] = ns[rg]; continue; }
+                    uint32_t yy = R < bt ? R : bt, nn = 0, xx = yy;
+                    if (R < bt && G && rg % HH_NR) yy = hh_region_head(&cf, R - G, R, nullptr);
+                    const uint32_t lim = R + S < bt ? R + S : bt;
+                    if (yy < lim) xx = hh_region_count(&cf, yy, lim, &nn);
+                    xr[k] = xx;
+                    nr[k] = nn;
+                }
                 const uint32_t g0 = (j + 1) * sw >= 2 ? (j + 1) * sw - 2 : 0;
                 const uint32_t nwin = 2 + HH_KM * sw + 4;
                 for (uint32_t q = 0; q < nwin; q++) win[(size_t)(g0 + q) * 64] = word_at(tw0 + g0 + q);
@@ -165,7 +179,16 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
                 cw.w = win.data();
                 cw.sw = 1024;
                 cw.nls = 64;
-                wk[j] = hh_walk(&cw, j, S, xs[j]);
+                const hh_wk we = hh_walk_exits(&cw, j, S, xs[j], xr, nr);
+                if (we.k != ref.k || (ref.k && (we.e != ref.e || we.cov != ref.cov || we.delta != ref.delta))) {
+                    fprintf(stderr, "emu: tile %lu lane %u exit walk (k %u e %u cov %u delta %d) vs mask walk (k %u e %u cov %u delta %d)\n",
+                            (unsigned long)t, j, we.k, we.e, we.cov, we.delta, ref.k, ref.e, ref.cov, ref.delta);
+                    return HH_ERR_INTERNAL - 502;
+                }
+                if (wk[j].more) {
+                    ndefer++;
+                    wk[j] = we;
+                }
             }
             if (wk[j].k != ref.k || (ref.k && (wk[j].e != ref.e || wk[j].cov != ref.cov || wk[j].delta != ref.delta))) {
                 fprintf(stderr, "emu: tile %lu lane %u walk (k %u e %u cov %u delta %d) vs mask walk (k %u e %u cov %u delta %d)\n",
