@@ -302,7 +302,7 @@ def main():
         "config": {"workload": workload + (f", sharded over {world} GPUs" if world > 1 else ", 1 MI355X"),
                    "compressed_bytes": C_all, "decoded_bytes": D_all,
                    "bits_per_gpu": int(C_bytes * 8), "parallelism": f"byte-range shards x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_front+k_scan1+k_scan2+k_emit",
+        "roofline": {"bound": "hbm", "kernel": "k_front+k_walk+k_table+k_scan1+k_scan2+k_emit",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_alg": C_bytes + D_bytes, "ms_kernel": round(ms_dev, 4),

@@ -74,7 +74,7 @@
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
                                  as a failed walk) */
 #ifndef HH_FRONT_WALK
-#define HH_FRONT_WALK 4       /* lookups of a walk in k_front; longer walks are
+#define HH_FRONT_WALK 2       /* lookups of a walk in k_front; longer walks are
                                  deferred to k_walk (a wave would wait for its
                                  longest walk) */
 #endif

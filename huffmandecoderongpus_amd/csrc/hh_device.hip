@@ -455,34 +455,46 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
 }
 
 // ---------------------------------------------------------------------------
-// k_walk: the deferred walks (k_front's lists), one lane each, over the
-// lane's own staging of the words it can reach: from G bits before region
-// j+1 to HH_KM regions further and a halo, at LDS index (g - g0) * 64 + lane
-// (a wave's lanes in distinct banks).  Exit comparisons (hh_walk_exits)
-// against the regions' pass-1 exits and counts (xn); the lane's record
-// replaces k_front's placeholder.
+// k_walk: the deferred walks (k_front's lists), one lane each: exit
+// comparisons (hh_walk_exits, restated here region by region) against the
+// regions' pass-1 exits and counts (xn).  A lane stages only the words of
+// the region it walks (from G bits before it, for the heads of regions that
+// were not decoded, to a halo past it) at LDS index (q * HH_WALK_T + lane),
+// double-buffered: region k+1's words are loaded while region k is walked.
+// The lane's record replaces k_front's placeholder.
 // ---------------------------------------------------------------------------
+#define HH_WALK_T 256
 template <uint32_t SW>
 struct WalkWin {
-    static constexpr uint32_t n = (2 + HH_KM * SW + 4 + 3 + 3) & ~3u;   // words (x4 loads from g0 & ~3)
+    static constexpr uint32_t n = SW + 6;   // words of one region's window
 };
 
 template <uint32_t SW>
-__global__ __launch_bounds__(64) void k_walk(const uint32_t *__restrict__ gdata, Geometry geo, DevTab tab, Work wk) {
+__device__ __forceinline__ void walk_win_load(uint32_t (&v)[WalkWin<SW>::n], const uint32_t *gdata, uint64_t gw0,
+                                              uint64_t glim) {
+#pragma unroll
+    for (uint32_t q = 0; q < WalkWin<SW>::n; q++) {
+        const uint64_t gi = gw0 + q;
+        v[q] = gdata[gi < glim ? gi : glim - 1];   // (past the payload: past the stream end, unused)
+    }
+}
+
+template <uint32_t SW>
+__global__ __launch_bounds__(HH_WALK_T) void k_walk(const uint32_t *__restrict__ gdata, Geometry geo, DevTab tab, Work wk) {
     extern __shared__ __align__(16) uint8_t smem[];
-    constexpr uint32_t S = 32 * SW, NWIN = WalkWin<SW>::n;
-    const uint32_t lane = threadIdx.x;
+    constexpr uint32_t S = 32 * SW, NW = WalkWin<SW>::n;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u;
     uint16_t *s_f = (uint16_t *)smem;                   // F, its escape directory, L2
     uint32_t *s_fdir = (uint32_t *)smem + HH_F_SIZE / 2;
     uint32_t *s_l2 = s_fdir + ((tab.fdir_used + 3u) & ~3u);
-    uint32_t *s_win = (uint32_t *)smem + ftab_words(tab.fdir_used, tab.l2_used);   // NWIN x 64 words
+    uint32_t *s_win = (uint32_t *)smem + ftab_words(tab.fdir_used, tab.l2_used) + tid;   // 2 x NW words
     load_ftables(tab, s_f, s_fdir, s_l2);
     __syncthreads();
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
     const uint32_t span = HH_NCOL * S;
     hh_ctx c;
-    c.sw = 1024;                                        // hh_idx(g) = g * 64: one column per lane
-    c.nls = 64;
+    c.sw = 1024;                                        // hh_idx(g) = g * HH_WALK_T (below)
+    c.nls = HH_WALK_T;
     c.magic = 0;
     c.l1m = nullptr;
     c.l1s = nullptr;
@@ -495,12 +507,14 @@ __global__ __launch_bounds__(64) void k_walk(const uint32_t *__restrict__ gdata,
     c.tsym = tab.tsym;
     c.maxadv = geo.maxadv > HH_PF ? geo.maxadv : HH_PF;
     c.G = geo.G;
-    // one k_front wave's list at a time, its entries over the lanes
-    uint32_t fw = blockIdx.x, i = lane, cnt = fw < geo.nfw ? wk.qn[fw] : 0u;
+    // one k_front wave's list at a time, its entries over the wave's lanes
+    const uint32_t nwv = gridDim.x * (HH_WALK_T / 64);
+    uint32_t fw = blockIdx.x * (HH_WALK_T / 64) + (tid >> 6), i = lane, cnt = fw < geo.nfw ? wk.qn[fw] : 0u;
+    uint32_t pre[NW];
     for (;;) {
         while (i >= cnt && fw < geo.nfw) {
             i -= cnt;
-            fw += gridDim.x;
+            fw += nwv;
             cnt = fw < geo.nfw ? wk.qn[fw] : 0u;
         }
         if (fw >= geo.nfw) break;
@@ -509,53 +523,55 @@ __global__ __launch_bounds__(64) void k_walk(const uint32_t *__restrict__ gdata,
         const uint64_t t = gl / HH_NR;
         const uint32_t j = gl % HH_NR;
         const uint32_t r0 = wk.xn[gl];
-        const uint32_t x = r0 & 0xffffu, n = r0 >> 16;
         const uint64_t rem = geo.bits - t * tile_bits;
         c.bt = rem < span ? (uint32_t)rem : span;
-        // exits and counts of regions j+1 .. j+HH_KM (the next tile's in its
-        // frame, + the tile's bits; past the decoded tiles: computed below)
-        uint32_t xr[HH_KM + 1], nr[HH_KM + 1], nmiss = 0;
-#pragma unroll
+        const uint32_t bt = c.bt;
+        const uint64_t tw0 = t * tile_bits / 32;
+        auto win0 = [&](uint32_t k) { const uint32_t g = (j + k) * SW; return g >= 2 ? g - 2 : 0u; };
+        walk_win_load<SW>(pre, gdata, tw0 + win0(1), geo.nwords);
+        uint32_t A = r0 & 0xffffu, ca = 0;
+        A = A < bt ? A : bt;
+        hh_wk w = {0u, 0u, 0u, 0, 0u, 0u};
         for (uint32_t k = 1; k <= HH_KM; k++) {
-            const uint32_t rg = j + k;
-            const bool nxt = rg >= HH_NR;
-            const bool have = !nxt || t + 1 < geo.ntiles;
-            const uint32_t v = have ? wk.xn[gl + k] : 0u;
-            xr[k] = (v & 0xffffu) + (nxt ? HH_NR * S : 0u);
-            nr[k] = v >> 16;
-            nmiss |= have ? 0u : 1u << k;
-        }
-        const uint32_t g0 = ((j + 1) * SW >= 2 ? (j + 1) * SW - 2 : 0u) & ~3u;
-        // plain loads (a buffer resource per lane would be a waterfall loop:
-        // one lane at a time); words past the payload are read clamped to
-        // its last readable ones -- they lie past the end of the stream,
-        // which no decision depends on
-        const uint64_t gw0 = t * tile_bits / 32 + g0, glim = geo.nwords;
+            const uint32_t sl = (k & 1u) * NW, g0 = win0(k);
 #pragma unroll
-        for (uint32_t q = 0; q < NWIN; q++) {
-            const uint64_t gi = gw0 + q;
-            s_win[q * 64 + lane] = gdata[gi < glim ? gi : glim - 1];
+            for (uint32_t q = 0; q < NW; q++) s_win[(sl + q) * HH_WALK_T] = pre[q];
+            if (k < HH_KM) walk_win_load<SW>(pre, gdata, tw0 + win0(k + 1), geo.nwords);
+            c.w = s_win + ((int32_t)sl - (int32_t)g0) * (int32_t)HH_WALK_T;   // tile word g at (sl + g - g0)
+            const uint32_t rg = j + k, R = rg * S;
+            const uint32_t Ec = R + S < bt ? R + S : bt;
+            // the region's own chain: its pass-1 exit and count (a tile past
+            // the decoded ones, at a range's end: decoded here)
+            uint32_t xk, nk;
+            if (rg < HH_NR || t + 1 < geo.ntiles) {
+                const uint32_t v = wk.xn[gl + k];
+                xk = (v & 0xffffu) + (rg >= HH_NR ? HH_NR * S : 0u);
+                nk = v >> 16;
+            } else {
+                uint32_t yy = R < bt ? R : bt;
+                nk = 0;
+                if (R < bt && c.G && rg % HH_NR) yy = hh_region_head(&c, R - c.G, R, nullptr);
+                xk = yy < Ec ? hh_region_count(&c, yy, Ec, &nk) : yy;
+            }
+            const uint32_t e = A > R ? A - R : 0u;
+            uint32_t n = 0;
+            if (A < Ec) A = hh_region_count(&c, A, Ec, &n);
+            if (A == (xk < bt ? xk : bt)) {
+                w.k = k;
+                w.e = e;
+                w.cov = ca;
+                w.delta = (int32_t)n - (int32_t)nk;
+                break;
+            }
+            ca += n;
         }
-        c.w = s_win + lane - g0 * 64;                   // (tile word g at (g - g0) * 64 + lane)
-        while (nmiss) {                                 // regions of a tile not decoded (a
-            const uint32_t k = __builtin_ctz(nmiss);    // range's end): their own pass 1
-            nmiss &= nmiss - 1;
-            const uint32_t rg = j + k, R = rg * S, bt = c.bt;
-            uint32_t yy = R < bt ? R : bt, nn = 0, xx = yy;
-            if (R < bt && c.G && rg % HH_NR) yy = hh_region_head(&c, R - c.G, R, nullptr);
-            const uint32_t lim = R + S < bt ? R + S : bt;
-            if (yy < lim) xx = hh_region_count(&c, yy, lim, &nn);
-            xr[k] = xx;
-            nr[k] = nn;
-        }
-        const hh_wk w = hh_walk_exits(&c, j, S, x, xr, nr);
         if (w.k == 0) {
             atomicOr(wk.flags, (uint32_t)F_FAIL);
             if (atomicCAS(&wk.flags[4], 0u, 1u) == 0u) {
-                wk.flags[5] = (uint32_t)t; wk.flags[6] = j; wk.flags[7] = x; wk.flags[8] = n; wk.flags[9] = c.bt;
+                wk.flags[5] = (uint32_t)t; wk.flags[6] = j; wk.flags[7] = r0 & 0xffffu; wk.flags[8] = r0 >> 16; wk.flags[9] = bt;
             }
         } else {
-            wk.recs[gl] = rec_pack(w.k, w.e, w.delta, n + w.cov);
+            wk.recs[gl] = rec_pack(w.k, w.e, w.delta, (r0 >> 16) + w.cov);
         }
     }
 }
@@ -1332,9 +1348,9 @@ static int stage_pipeline(hh_decoder *d, const void *d_data, int64_t bits, uint8
 static size_t lds_front(uint32_t sw, uint32_t l2, uint32_t fdir) {
     return ((size_t)ftab_words(fdir, l2) + (size_t)HH_FW * sw * HH_NLS) * 4;
 }
-static uint32_t walk_win(uint32_t sw) { return (2 + HH_KM * sw + 4 + 3 + 3) & ~3u; }   // WalkWin<sw>::n
+static uint32_t walk_win(uint32_t sw) { return sw + 6; }   // WalkWin<sw>::n
 static size_t lds_walk(uint32_t sw, uint32_t l2, uint32_t fdir) {
-    return ((size_t)ftab_words(fdir, l2) + (size_t)walk_win(sw) * 64) * 4;
+    return ((size_t)ftab_words(fdir, l2) + (size_t)2 * walk_win(sw) * HH_WALK_T) * 4;
 }
 static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree) {
     return (2 * (size_t)HH_L1_SIZE + (size_t)HH_NW * sw * HH_NLS + l2) * 4 + (size_t)HH_NW * HH_OBW +
@@ -1376,7 +1392,7 @@ static int size_grids(hh_decoder *d, uint32_t sw) {
         return HH_OK;
     int pf = 0, pe = 0, pw = 0, ncu = 0;
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pf, kfront_for(sw), 64 * HH_FW, lds_front(sw, d->tab.l2_used, d->tab.fdir_used)));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, kwalk_for(sw), 64, lds_walk(sw, d->tab.l2_used, d->tab.fdir_used)));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, kwalk_for(sw), HH_WALK_T, lds_walk(sw, d->tab.l2_used, d->tab.fdir_used)));
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kemit_for(sw), HH_NL, lds_emit(sw, d->tab.l2_used, d->tab.tree_lds)));
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
     if (pf < 1 || pe < 1 || pw < 1) return HH_ERR_UNSUPPORTED;
@@ -1511,7 +1527,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
                        (const uint32_t *)d_data, geo, d->tab, wk, d->d_dbg);
     HIP_OK(hipGetLastError());
     // the deferred walks (their count is on the device: a persistent grid)
-    hipLaunchKernelGGL(kw, dim3(d->grid_w), dim3(64), lds_walk(geo.sw, d->tab.l2_used, d->tab.fdir_used), st,
+    hipLaunchKernelGGL(kw, dim3(d->grid_w), dim3(HH_WALK_T), lds_walk(geo.sw, d->tab.l2_used, d->tab.fdir_used), st,
                        (const uint32_t *)d_data, geo, d->tab, wk);
     HIP_OK(hipGetLastError());
     {
