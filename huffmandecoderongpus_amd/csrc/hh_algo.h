@@ -74,9 +74,10 @@
 #define HH_WALK_MAX 8192      /* iteration cap of one walk (a guard, reported
                                  as a failed walk) */
 #ifndef HH_FRONT_WALK
-#define HH_FRONT_WALK 2       /* lookups of a walk in k_front; longer walks are
+#define HH_FRONT_WALK 0       /* lookups of a walk in k_front; longer walks are
                                  deferred to k_walk (a wave would wait for its
-                                 longest walk) */
+                                 longest walk; 0, 1, 2, 4: kjv front + walks
+                                 1.33, 1.37, 1.42, 1.49 ms per GiB) */
 #endif
 
 HH_HD uint32_t hh_umulhi(uint32_t a, uint32_t b) {

@@ -51,6 +51,9 @@
 #endif
 #define HH_SCAN_TB 1024             // tiles per k_scan1 block
 #define HH_SCAN_BACK 4096           // longest non-CONST chain k_scan1 composes (else host scan)
+#ifndef HH_XPT
+#define HH_XPT 4                    // k_emit: deferred runs per tile a wave's list holds
+#endif
 #define HH_OBW (4096 + 64)          // k_emit's LDS output staging per wave (bytes): a text tile's
                                     // output (~3.7 K symbols for kjv) plus the 16-B phase
 
@@ -110,6 +113,7 @@ struct Geometry {
     uint32_t fwalk;      // lookups of a walk in k_front (longer: deferred to k_walk)
     uint32_t nfw;        // k_front's waves (each with its list of deferred walks)
     uint64_t qcap;       // entries per list (the wave's tiles x HH_NR)
+    uint32_t xcap;       // k_emit: deferred runs per wave's list (HH_XPT per tile)
 };
 
 // Workspace carve (decode_fast).  Nothing but `flags` needs zeroing: every
@@ -124,6 +128,8 @@ struct Work {
     uint32_t *q;         // [nfw][qcap] deferred walks of each k_front wave (tile * HH_NR + lane)
     uint32_t *qn;        // [nfw] their counts
     uint32_t *xn;        // [ntiles * HH_NR] pass-1 exit | count << 16 of every region
+    uint64_t *xq;        // [k_emit waves][xcap] deferred runs: output offset, tile << 32 | entry | end << 16
+    uint32_t *xqn;       // [k_emit waves] their counts
 };
 
 // ---------------------------------------------------------------------------
@@ -405,7 +411,10 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
         // walks: region j's exit against the next regions' own chains, two
         // pointers, at most geo.fwalk lookups here
         hh_wk w = {1u, x - R1, 0u, 0, 0u, 0u};
-        if (!merged) w = hh_walk(&c, j, S, x, nullptr, nullptr, nullptr, 0, geo.fwalk, s_y, HH_NR);
+        if (!merged) {
+            if (geo.fwalk) w = hh_walk(&c, j, S, x, nullptr, nullptr, nullptr, 0, geo.fwalk, s_y, HH_NR);
+            else w.more = 1u;                           // (every walk to k_walk)
+        }
         const uint32_t rec = rec_pack(w.k ? w.k : 1u, w.e, w.delta, n + w.cov);
         if (w.more) {
             const uint64_t dm = __ballot(1);            // (the deferring lanes)
@@ -738,6 +747,57 @@ __global__ __launch_bounds__(1024) void k_scan2(Geometry geo, Work wk, uint32_t 
 }
 
 // ---------------------------------------------------------------------------
+// A run [cu.p, pe) of the true chain decoded straight to HBM at dst: bytes up
+// to a dword boundary, then dwords, then the ragged end (the first and last
+// dwords may be shared with the neighbouring runs).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void emit_run_direct(const hh_ctx *c, hh_cur cu, uint32_t pe, uint8_t *dst,
+                                                uint32_t maxadv) {
+    uint32_t o = 0, val, k;
+    while ((((uintptr_t)dst + o) & 3u) && cu.p < pe) {
+        const uint32_t ha = o + (4u - (uint32_t)(((uintptr_t)dst + o) & 3u));
+        hh_emit_step(c, cu, pe, o, ha, &val, &k);
+        for (uint32_t i = 0; i < k; i++) dst[o + i] = (uint8_t)(val >> (8 * i));
+        o += k;
+    }
+    uint64_t acc = 0;
+    uint32_t nacc = 0;
+    // whole lookups while the longest possible one still ends by pe
+    const uint32_t pf_end = pe > maxadv ? pe - maxadv : 0u;
+    while (cu.p < pf_end) {
+        const uint32_t win = hh_cur_win(cu);
+        const uint64_t le = c->l1[win & (HH_L1_SIZE - 1u)];
+        const uint32_t m = (uint32_t)(le >> 32);
+        uint32_t sy = (uint32_t)le, ns = HH_M_NSYM(m), nb = HH_M_NBITS(m);
+        if (ns == 0) {
+            nb = hh_escape(c, cu.p, win, m, &sy);
+            ns = 1;
+        }
+        acc |= (uint64_t)sy << (8 * nacc);
+        nacc += ns;
+        if (nacc >= 4) {
+            *(uint32_t *)(dst + o) = (uint32_t)acc;
+            acc >>= 32;
+            nacc -= 4;
+            o += 4;
+        }
+        hh_cur_adv(c, cu, nb);
+    }
+    while (cu.p < pe) {
+        hh_emit_step(c, cu, pe, o + nacc, ~0ull, &val, &k);
+        acc |= (uint64_t)val << (8 * nacc);
+        nacc += k;
+        if (nacc >= 4) {
+            *(uint32_t *)(dst + o) = (uint32_t)acc;
+            acc >>= 32;
+            nacc -= 4;
+            o += 4;
+        }
+    }
+    for (uint32_t i = 0; i < nacc; i++) dst[o + i] = (uint8_t)(acc >> (8 * i));
+}
+
+// ---------------------------------------------------------------------------
 // k_emit: pass 2 of every emitted tile, one tile per wave at a time (wave gw
 // takes tiles f0 + gw, f0 + gw + #waves, ...; f0 = emit_from).  Like
 // k_front, a wave never waits for another: its tile's words, live lanes,
@@ -815,6 +875,8 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
         prefetch_wtile<SW>(pf, gdata, tt * tile_bits / 32, geo.nwords);
     };
     uint64_t t = f0 + (uint64_t)blockIdx.x * HH_NW + wv;
+    const uint32_t gwe = blockIdx.x * HH_NW + wv;       // this wave's list of deferred runs
+    uint32_t xqn = 0;
     if (t < geo.ntiles) prefetch_next(t);
     EDIAG_DECL
     for (; t < geo.ntiles; t += nwv) {
@@ -858,7 +920,26 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
 
         hh_cur cu = hh_cur_at(&c, live ? e_in : 0u);
         const uint32_t y = (j + kk) * S + ee;
-        const uint32_t pe = (live && fits) ? (y < bt ? y : bt) : 0u;
+        uint32_t pe = (live && fits) ? (y < bt ? y : bt) : 0u;
+        {
+            // A run over several regions (a walk that crossed them) would hold
+            // up the wave for as many regions: it goes to the wave's list for
+            // k_emitx (lane-parallel), unless the list is full.  Its bytes
+            // are copied out as zeros here and written by k_emitx after.
+            const bool want = kk > 1 && cu.p < pe;
+            const uint64_t dm = __ballot(want);
+            const uint32_t nd = (uint32_t)__builtin_popcountll(dm);
+            if (nd && xqn + nd <= geo.xcap) {
+                if (want) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
+                    uint64_t *xe = wk.xq + 2 * ((uint64_t)gwe * geo.xcap + xqn + rank);
+                    xe[0] = P0 + L;
+                    xe[1] = (t << 32) | cu.p | (pe << 16);
+                    pe = 0;
+                }
+                xqn += nd;
+            }
+        }
         // The tile's output [P0, P0 + Tout) is staged in the wave's LDS at
         // byte a0 = P0 mod 16, so that 16-B blocks of LDS and of HBM line
         // up: lanes OR their symbols in as dwords (a dword two runs share
@@ -889,12 +970,21 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
                     acc |= (uint64_t)sy << (8 * nacc);
                     nacc += ns;
                     emitted += ns;
+#ifdef HH_EXP_ORALL
+                    // every step ORs the open dword (idempotent), no branch
+                    atomicOr(&s_out[wd], (uint32_t)acc);
+                    const bool full = nacc >= 4;
+                    wd += full ? 1u : 0u;
+                    acc = full ? acc >> 32 : acc;
+                    nacc -= full ? 4u : 0u;
+#else
                     if (nacc >= 4) {
                         atomicOr(&s_out[wd], (uint32_t)acc);
                         wd++;
                         acc >>= 32;
                         nacc -= 4;
                     }
+#endif
                     hh_cur_adv(&c, cu, nb);
                 }
                 while (cu.p < pe) {                // the end of the run (and of the stream)
@@ -932,57 +1022,74 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
             continue;
         }
         // a tile too large for the staging buffer: this lane's symbols
-        // straight to HBM (output bytes [P0 + L, P0 + L + rc)); bytes up to a
-        // dword boundary, then dwords, then the ragged end
-        if (cu.p < pe) {
-            uint8_t *ob = out + P0;
-            uint32_t o = L, val, k;
-            const uint32_t oend = L + rc;
-            while (((P0 + o) & 3u) && cu.p < pe) {
-                const uint32_t ha = o + (4u - (uint32_t)((P0 + o) & 3u));
-                hh_emit_step(&c, cu, pe, o, ha, &val, &k);
-                for (uint32_t i = 0; i < k; i++) ob[o + i] = (uint8_t)(val >> (8 * i));
-                o += k;
-            }
-            uint64_t acc = 0;
-            uint32_t nacc = 0;
-            // whole lookups while the longest possible one still ends by pe
-            const uint32_t pf_end = pe > geo.maxadv ? pe - geo.maxadv : 0u;
-            while (cu.p < pf_end) {
-                const uint32_t win = hh_cur_win(cu);
-                const uint32_t ix = win & (HH_L1_SIZE - 1u);
-                const uint64_t le = s_l1[ix];
-                const uint32_t m = (uint32_t)(le >> 32);
-                uint32_t sy = (uint32_t)le, ns = HH_M_NSYM(m), nb = HH_M_NBITS(m);
-                if (ns == 0) {
-                    nb = hh_escape(&c, cu.p, win, m, &sy);
-                    ns = 1;
-                }
-                acc |= (uint64_t)sy << (8 * nacc);
-                nacc += ns;
-                if (nacc >= 4) {
-                    *(uint32_t *)(ob + o) = (uint32_t)acc;
-                    acc >>= 32;
-                    nacc -= 4;
-                    o += 4;
-                }
-                hh_cur_adv(&c, cu, nb);
-            }
-            while (cu.p < pe) {
-                hh_emit_step(&c, cu, pe, o + nacc, oend, &val, &k);
-                acc |= (uint64_t)val << (8 * nacc);
-                nacc += k;
-                if (nacc >= 4) {
-                    *(uint32_t *)(ob + o) = (uint32_t)acc;
-                    acc >>= 32;
-                    nacc -= 4;
-                    o += 4;
-                }
-            }
-            for (uint32_t i = 0; i < nacc; i++) ob[o + i] = (uint8_t)(acc >> (8 * i));
-        }
+        // straight to HBM (output bytes [P0 + L, P0 + L + rc))
+        if (cu.p < pe) emit_run_direct(&c, cu, pe, out + P0 + L, geo.maxadv);
     }
+    if (j == 0) wk.xqn[gwe] = xqn;
     EDIAG_FLUSH(dbg);
+}
+
+// ---------------------------------------------------------------------------
+// k_emitx: the runs k_emit deferred (several regions long), one lane each,
+// over the lane's own staging of the run's words at LDS index
+// (g - g0) * 64 + lane; straight to HBM (emit_run_direct).
+// ---------------------------------------------------------------------------
+template <uint32_t SW>
+struct EmitxWin {
+    static constexpr uint32_t n = (HH_KM + 1) * SW + 6;
+};
+
+template <uint32_t SW>
+__global__ __launch_bounds__(64) void k_emitx(const uint32_t *__restrict__ gdata, Geometry geo, DevTab tab, Work wk,
+                                              uint8_t *__restrict__ out, uint32_t nwe) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr uint32_t S = 32 * SW, NW = EmitxWin<SW>::n;
+    const uint32_t lane = threadIdx.x;
+    uint64_t *s_l1 = (uint64_t *)smem;
+    uint32_t *s_l2 = (uint32_t *)(s_l1 + HH_L1_SIZE);
+    uint32_t *s_win = s_l2 + ((tab.l2_used + 3u) & ~3u) + lane;   // NW x 64 words
+    for (uint32_t i = lane; i < HH_L1_SIZE; i += 64) s_l1[i] = tab.l1[i];
+    for (uint32_t i = lane; i < tab.l2_used; i += 64) s_l2[i] = tab.l2[i];
+    __syncthreads();
+    const uint64_t tile_bits = (uint64_t)HH_NR * S;
+    const uint32_t span = HH_NCOL * S;
+    hh_ctx c;
+    c.sw = 1024;                                        // hh_idx(g) = g * 64 (below)
+    c.nls = 64;
+    c.magic = 0;
+    c.l1m = nullptr;
+    c.l1s = nullptr;
+    c.l1 = s_l1;
+    c.l2 = s_l2;
+    c.tree = tab.tree;
+    c.tsym = tab.tsym;
+    c.maxadv = geo.maxadv;
+    c.G = geo.G;
+    uint32_t fw = blockIdx.x, i = lane, cnt = fw < nwe ? wk.xqn[fw] : 0u;
+    for (;;) {
+        while (i >= cnt && fw < nwe) {
+            i -= cnt;
+            fw += gridDim.x;
+            cnt = fw < nwe ? wk.xqn[fw] : 0u;
+        }
+        if (fw >= nwe) break;
+        const uint64_t *xe = wk.xq + 2 * ((uint64_t)fw * geo.xcap + i);
+        i += 64;
+        const uint64_t O = xe[0], w1 = xe[1];
+        const uint64_t t = w1 >> 32;
+        const uint32_t e_in = (uint32_t)w1 & 0xffffu, pe = ((uint32_t)w1 >> 16) & 0xffffu;
+        const uint64_t rem = geo.bits - t * tile_bits;
+        c.bt = rem < span ? (uint32_t)rem : span;
+        const uint32_t g0 = e_in >> 5;
+        const uint64_t gw0 = t * tile_bits / 32 + g0, glim = geo.nwords;
+#pragma unroll 8
+        for (uint32_t q = 0; q < NW; q++) {
+            const uint64_t gi = gw0 + q;
+            s_win[q * 64] = gdata[gi < glim ? gi : glim - 1];
+        }
+        c.w = s_win - (int32_t)(g0 * 64);
+        emit_run_direct(&c, hh_cur_at(&c, e_in), pe, out + O, geo.maxadv);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1182,7 +1289,7 @@ struct hh_decoder {
     uint64_t *d_dbg;     // HH_DIAG counters (16 x u64)
     hipEvent_t ev[4];
     hh_stats stats;
-    uint32_t grid_f, grid_e, grid_w;   // persistent grid sizes (occupancy x CUs)
+    uint32_t grid_f, grid_e, grid_w, grid_x;   // persistent grid sizes (occupancy x CUs)
     uint32_t fwalk;            // k_front's walk bound (HH_FRONT_WALK overrides)
     uint32_t ncu;              // compute units
     uint32_t grid_sw;          // words per region they were sized for
@@ -1352,6 +1459,9 @@ static uint32_t walk_win(uint32_t sw) { return sw + 6; }   // WalkWin<sw>::n
 static size_t lds_walk(uint32_t sw, uint32_t l2, uint32_t fdir) {
     return ((size_t)ftab_words(fdir, l2) + (size_t)2 * walk_win(sw) * HH_WALK_T) * 4;
 }
+static size_t lds_emitx(uint32_t sw, uint32_t l2) {
+    return (size_t)HH_L1_SIZE * 8 + (size_t)((l2 + 3) & ~3u) * 4 + (size_t)((HH_KM + 1) * sw + 6) * 64 * 4;
+}
 static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree) {
     return (2 * (size_t)HH_L1_SIZE + (size_t)HH_NW * sw * HH_NLS + l2) * 4 + (size_t)HH_NW * HH_OBW +
            (size_t)tree * 5;
@@ -1376,6 +1486,15 @@ static kwalk_t kwalk_for(uint32_t sw) {
     default: return nullptr;
     }
 }
+typedef void (*kemitx_t)(const uint32_t *, Geometry, DevTab, Work, uint8_t *, uint32_t);
+static kemitx_t kemitx_for(uint32_t sw) {
+    switch (sw) {
+#define X(n) case n: return k_emitx<n>;
+        HH_SW_CASES(X)
+#undef X
+    default: return nullptr;
+    }
+}
 static kemit_t kemit_for(uint32_t sw) {
     switch (sw) {
 #define X(n) case n: return k_emit<n>;
@@ -1390,14 +1509,16 @@ static int size_grids(hh_decoder *d, uint32_t sw) {
     if (d->grid_f && d->grid_sw == sw && d->grid_l2 == d->tab.l2_used && d->grid_tree == d->tab.tree_lds &&
         d->grid_fdir == d->tab.fdir_used)
         return HH_OK;
-    int pf = 0, pe = 0, pw = 0, ncu = 0;
+    int pf = 0, pe = 0, pw = 0, px = 0, ncu = 0;
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pf, kfront_for(sw), 64 * HH_FW, lds_front(sw, d->tab.l2_used, d->tab.fdir_used)));
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, kwalk_for(sw), HH_WALK_T, lds_walk(sw, d->tab.l2_used, d->tab.fdir_used)));
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&px, kemitx_for(sw), 64, lds_emitx(sw, d->tab.l2_used)));
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kemit_for(sw), HH_NL, lds_emit(sw, d->tab.l2_used, d->tab.tree_lds)));
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
-    if (pf < 1 || pe < 1 || pw < 1) return HH_ERR_UNSUPPORTED;
+    if (pf < 1 || pe < 1 || pw < 1 || px < 1) return HH_ERR_UNSUPPORTED;
     d->grid_f = (uint32_t)(pf * ncu);
     d->grid_w = (uint32_t)(pw * ncu);
+    d->grid_x = (uint32_t)(px * ncu);
     d->ncu = (uint32_t)ncu;
     d->grid_e = (uint32_t)(pe * ncu);
     d->grid_sw = sw;
@@ -1496,7 +1617,13 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     geo.qcap = (nt + geo.nfw - 1) / geo.nfw * HH_NR;
     const size_t o_qn = o_blk + (size_t)nblk * 8, o_q = o_qn + (size_t)geo.nfw * 4;
     const size_t o_xn = o_q + (size_t)geo.nfw * geo.qcap * 4;
-    const size_t need = o_xn + nt * HH_NR * 4;
+    const uint64_t ne = nt > emit_from ? nt - emit_from : 0;
+    const uint64_t ng = (ne + HH_NW - 1) / HH_NW;          // workgroups' worth of tiles
+    const uint32_t ge = (uint32_t)(ng < d->grid_e ? (ng ? ng : 1) : d->grid_e);
+    const uint32_t nwe = ge * HH_NW;                        // k_emit's waves
+    geo.xcap = (uint32_t)((ne + nwe - 1) / nwe * HH_XPT);
+    const size_t o_xqn = o_xn + nt * HH_NR * 4, o_xq = (o_xqn + (size_t)nwe * 4 + 15) & ~(size_t)15;
+    const size_t need = o_xq + (size_t)nwe * geo.xcap * 16;
     rc = ensure_dev(&d->ws, &d->ws_size, need);
     if (rc) return rc;
     uint8_t *w = (uint8_t *)d->ws;
@@ -1510,13 +1637,23 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     wk.q = (uint32_t *)(w + o_q);
     wk.qn = (uint32_t *)(w + o_qn);
     wk.xn = (uint32_t *)(w + o_xn);
+    wk.xqn = (uint32_t *)(w + o_xqn);
+    wk.xq = (uint64_t *)(w + o_xq);
     const kfront_t kf = kfront_for(geo.sw);
     const kwalk_t kw = kwalk_for(geo.sw);
     const kemit_t ke = kemit_for(geo.sw);
-    if (!kf || !kw || !ke) return HH_ERR_UNSUPPORTED;
-    const uint64_t ne = nt > emit_from ? nt - emit_from : 0;
-    const uint64_t ng = (ne + HH_NW - 1) / HH_NW;          // workgroups' worth of tiles
-    const uint32_t ge = (uint32_t)(ng < d->grid_e ? (ng ? ng : 1) : d->grid_e);
+    const kemitx_t kx = kemitx_for(geo.sw);
+    if (!kf || !kw || !ke || !kx) return HH_ERR_UNSUPPORTED;
+    // k_emit, then the runs it deferred
+    auto launch_emit = [&]() -> int {
+        hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds), st,
+                           (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap, d->d_dbg);
+        HIP_OK(hipGetLastError());
+        hipLaunchKernelGGL(kx, dim3(d->grid_x), dim3(64), lds_emitx(geo.sw, d->tab.l2_used), st,
+                           (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, nwe);
+        HIP_OK(hipGetLastError());
+        return HH_OK;
+    };
 
     HIP_OK(hipMemsetAsync(wk.flags, 0, 64, st));
 #ifdef HH_DIAG
@@ -1542,11 +1679,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     hipLaunchKernelGGL(k_scan2, dim3(1), dim3(1024), 0, st, geo, wk, nblk);
     HIP_OK(hipGetLastError());
     HIP_OK(hipEventRecord(d->ev[2], st));
-    if (ne) {
-        hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds), st,
-                           (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap, d->d_dbg);
-        HIP_OK(hipGetLastError());
-    }
+    if (ne && (rc = launch_emit())) return rc;
     HIP_OK(hipEventRecord(d->ev[3], st));
     HIP_OK(hipMemcpyAsync(d->h_flags, wk.flags, 64, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -1554,11 +1687,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
         // a non-CONST chain too long for k_scan1: compose on the host, emit again
         rc = scan_host(d, geo, wk, nblk, st);
         if (rc) return rc;
-        if (ne) {
-            hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds), st,
-                               (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap, d->d_dbg);
-            HIP_OK(hipGetLastError());
-        }
+        if (ne && (rc = launch_emit())) return rc;
         HIP_OK(hipEventRecord(d->ev[3], st));
         HIP_OK(hipMemcpyAsync(d->h_flags, wk.flags, 64, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
