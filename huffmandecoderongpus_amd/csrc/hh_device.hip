@@ -125,7 +125,8 @@ struct Work {
     uint32_t *st;        // [ntiles + 1] state entering each tile (st[ntiles]: leaving the last)
     int32_t *lex;        // [ntiles + 1] exclusive prefix of charged counts within its scan block
     int64_t *blk;        // [nblk] scan block totals, then exclusive block bases
-    uint32_t *q;         // [nfw][qcap] deferred walks of each k_front wave (tile * HH_NR + lane)
+    uint64_t *q;         // [nfw][qcap] deferred walks of each k_front wave: tile * HH_NR + lane |
+                         // (exit | count << 16) << 32
     uint32_t *qn;        // [nfw] their counts
     uint32_t *xn;        // [ntiles * HH_NR] pass-1 exit | count << 16 of every region
     uint64_t *xq;        // [k_emit waves][xcap] deferred runs: output offset, tile << 32 | entry | end << 16
@@ -419,7 +420,7 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
         if (w.more) {
             const uint64_t dm = __ballot(1);            // (the deferring lanes)
             const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u));
-            wk.q[qbase + qn + rank] = (uint32_t)(t * HH_NR + j);
+            wk.q[qbase + qn + rank] = (uint64_t)(t * HH_NR + j) | ((uint64_t)(x | (n << 16)) << 32);
         }
         {
             // the wave's own list (an atomic on one counter per deferring
@@ -516,28 +517,43 @@ __global__ __launch_bounds__(HH_WALK_T) void k_walk(const uint32_t *__restrict__
     c.tsym = tab.tsym;
     c.maxadv = geo.maxadv > HH_PF ? geo.maxadv : HH_PF;
     c.G = geo.G;
-    // one k_front wave's list at a time, its entries over the wave's lanes
+    // one k_front wave's list at a time, its entries over the wave's lanes;
+    // the next entry is loaded one walk ahead
     const uint32_t nwv = gridDim.x * (HH_WALK_T / 64);
     uint32_t fw = blockIdx.x * (HH_WALK_T / 64) + (tid >> 6), i = lane, cnt = fw < geo.nfw ? wk.qn[fw] : 0u;
-    uint32_t pre[NW];
-    for (;;) {
+    auto next_entry = [&](uint64_t &e) -> bool {
         while (i >= cnt && fw < geo.nfw) {
             i -= cnt;
             fw += nwv;
             cnt = fw < geo.nfw ? wk.qn[fw] : 0u;
         }
-        if (fw >= geo.nfw) break;
-        const uint32_t gl = wk.q[(uint64_t)fw * geo.qcap + i];
+        if (fw >= geo.nfw) return false;
+        e = wk.q[(uint64_t)fw * geo.qcap + i];
         i += 64;
+        return true;
+    };
+    uint32_t pre[NW];
+    uint64_t en = 0;
+    bool have_n = next_entry(en);
+    while (have_n) {
+        const uint64_t ent = en;
+        have_n = next_entry(en);
+        const uint32_t gl = (uint32_t)ent;
         const uint64_t t = gl / HH_NR;
         const uint32_t j = gl % HH_NR;
-        const uint32_t r0 = wk.xn[gl];
+        const uint32_t r0 = (uint32_t)(ent >> 32);
         const uint64_t rem = geo.bits - t * tile_bits;
         c.bt = rem < span ? (uint32_t)rem : span;
         const uint32_t bt = c.bt;
         const uint64_t tw0 = t * tile_bits / 32;
         auto win0 = [&](uint32_t k) { const uint32_t g = (j + k) * SW; return g >= 2 ? g - 2 : 0u; };
         walk_win_load<SW>(pre, gdata, tw0 + win0(1), geo.nwords);
+        // the regions' pass-1 exits and counts, all loaded at once (a tile
+        // past the decoded ones, at a range's end: decoded below)
+        const bool nxt_ok = t + 1 < geo.ntiles;
+        uint32_t xv[HH_KM + 1];
+#pragma unroll
+        for (uint32_t k = 1; k <= HH_KM; k++) xv[k] = wk.xn[gl + k];   // (xn has a tile of slack)
         uint32_t A = r0 & 0xffffu, ca = 0;
         A = A < bt ? A : bt;
         hh_wk w = {0u, 0u, 0u, 0, 0u, 0u};
@@ -552,8 +568,8 @@ __global__ __launch_bounds__(HH_WALK_T) void k_walk(const uint32_t *__restrict__
             // the region's own chain: its pass-1 exit and count (a tile past
             // the decoded ones, at a range's end: decoded here)
             uint32_t xk, nk;
-            if (rg < HH_NR || t + 1 < geo.ntiles) {
-                const uint32_t v = wk.xn[gl + k];
+            if (rg < HH_NR || nxt_ok) {
+                const uint32_t v = xv[k];
                 xk = (v & 0xffffu) + (rg >= HH_NR ? HH_NR * S : 0u);
                 nk = v >> 16;
             } else {
@@ -1292,6 +1308,7 @@ struct hh_decoder {
     uint32_t grid_f, grid_e, grid_w, grid_x;   // persistent grid sizes (occupancy x CUs)
     uint32_t fwalk;            // k_front's walk bound (HH_FRONT_WALK overrides)
     uint32_t ncu;              // compute units
+    uint32_t xpt;              // k_emit's deferred runs per tile (HH_EMIT_XPT overrides)
     uint32_t grid_sw;          // words per region they were sized for
     size_t grid_l2;            // and the L2 table size
     uint32_t grid_tree;        // and the LDS tree size
@@ -1422,8 +1439,11 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     d->tab.tree_lds = d->ht->tree_used;
     d->S = pick_region_bits(d->ht, d->cfg.lane_bits);
     d->fwalk = HH_FRONT_WALK;
-    const char *fw = getenv("HH_FRONT_WALK");            // experiments
+    const char *fw = getenv("HH_FRONT_WALK");            // experiments, tests
     if (fw && *fw) d->fwalk = (uint32_t)atoi(fw);
+    d->xpt = HH_XPT;
+    const char *xp = getenv("HH_EMIT_XPT");
+    if (xp && *xp) d->xpt = (uint32_t)atoi(xp);
     d->G = hh_pick_overlap(d->ht);
     if (getenv("HH_OVERLAP")) d->G = (uint32_t)atoi(getenv("HH_OVERLAP")) & ~31u;   // experiments
     if (d->G > HH_GMAX || d->G + 32 > d->S) d->G = 0;
@@ -1615,14 +1635,14 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     const uint32_t gf = (uint32_t)(nfw < d->grid_f ? nfw : d->grid_f);
     geo.nfw = gf * HH_FW;
     geo.qcap = (nt + geo.nfw - 1) / geo.nfw * HH_NR;
-    const size_t o_qn = o_blk + (size_t)nblk * 8, o_q = o_qn + (size_t)geo.nfw * 4;
-    const size_t o_xn = o_q + (size_t)geo.nfw * geo.qcap * 4;
+    const size_t o_qn = o_blk + (size_t)nblk * 8, o_q = (o_qn + (size_t)geo.nfw * 4 + 7) & ~(size_t)7;
+    const size_t o_xn = o_q + (size_t)geo.nfw * geo.qcap * 8;
     const uint64_t ne = nt > emit_from ? nt - emit_from : 0;
     const uint64_t ng = (ne + HH_NW - 1) / HH_NW;          // workgroups' worth of tiles
     const uint32_t ge = (uint32_t)(ng < d->grid_e ? (ng ? ng : 1) : d->grid_e);
     const uint32_t nwe = ge * HH_NW;                        // k_emit's waves
-    geo.xcap = (uint32_t)((ne + nwe - 1) / nwe * HH_XPT);
-    const size_t o_xqn = o_xn + nt * HH_NR * 4, o_xq = (o_xqn + (size_t)nwe * 4 + 15) & ~(size_t)15;
+    geo.xcap = (uint32_t)((ne + nwe - 1) / nwe * d->xpt);
+    const size_t o_xqn = o_xn + (nt + 1) * HH_NR * 4, o_xq = (o_xqn + (size_t)nwe * 4 + 15) & ~(size_t)15;
     const size_t need = o_xq + (size_t)nwe * geo.xcap * 16;
     rc = ensure_dev(&d->ws, &d->ws_size, need);
     if (rc) return rc;
@@ -1634,7 +1654,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     wk.st = (uint32_t *)(w + o_st);
     wk.lex = (int32_t *)(w + o_lex);
     wk.blk = (int64_t *)(w + o_blk);
-    wk.q = (uint32_t *)(w + o_q);
+    wk.q = (uint64_t *)(w + o_q);
     wk.qn = (uint32_t *)(w + o_qn);
     wk.xn = (uint32_t *)(w + o_xn);
     wk.xqn = (uint32_t *)(w + o_xqn);

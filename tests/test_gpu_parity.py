@@ -206,6 +206,35 @@ def test_synthetic_full_size(hh, files_dir, src, mib):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("env", [{"HH_FRONT_WALK": "2"}, {"HH_FRONT_WALK": "16"},
+                                 {"HH_FRONT_WALK": "8192"}, {"HH_EMIT_XPT": "0"},
+                                 {"HH_EMIT_XPT": "1"}])
+def test_walk_bound_and_deferral_lists(hh, files_dir, env, monkeypatch):
+    """The work the fast path moves out of its waves -- walks longer than
+    the front's bound (to k_walk), runs over several regions (to k_emitx,
+    through per-wave lists that may fill up) -- must give the same bytes
+    whichever part of it moves: every walk in k_front (8192), a few, none
+    (0, the default); no run deferred (0), lists that overflow (1)."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)                # read when the tree is set
+    hf, text = synth.load_source(files_dir, "kjv.txt")
+    syn = synth.tiled_stream(hf, text, 64 << 20)
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(syn.tree)
+        out = torch.full((syn.decoded_bytes + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+        n = dec.decode_device(syn.data, syn.bits, out)
+        torch.cuda.synchronize()
+        assert n == syn.decoded_bytes
+        assert synth.verify_tiled(out, syn)
+        assert int(out[n:n + 64].ne(0xAB).sum()) == 0
+        assert dec.stats()["exact_fallback"] == 0
+    finally:
+        dec.close()
+
+
 @pytest.mark.parametrize("mib", [64, 1024])
 def test_iid_stream(hh, files_dir, mib):
     """SURVEY 8d's i.i.d. variant: kjv unigram symbols from splitmix64 (seed
