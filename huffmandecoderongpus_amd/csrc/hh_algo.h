@@ -99,7 +99,7 @@ HH_HD uint32_t hh_lowmask(uint32_t o) { return o >= 32 ? 0xffffffffu : ((1u << o
 #define HH_M_NBITS(m) ((m) & 31u)
 #define HH_M_NSYM(m) (((m) >> 5) & 7u)
 #define HH_M_LEN0(m) (((m) >> 8) & 31u)
-#define HH_M_BMASK(m) (((m) >> 13) & 0x7ffu)
+#define HH_M_BMASK(m) (((m) >> 13) & ((1u << HH_P) - 1u))
 /* escape meta word (nsym == 0): the L2 subtable */
 #define HH_M_L2BASE(m) (((m) >> 8) & 0xffffu)
 #define HH_M_L2Q(m) (((m) >> 24) & 31u)

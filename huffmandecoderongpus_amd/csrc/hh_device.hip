@@ -40,11 +40,11 @@
 #include "hiphuff.h"
 
 #define HH_MAXLEN_FAST 32           // longest code of the fast path (one cursor step <= 32 bits)
-#ifndef HH_NL
-#define HH_NL 512                   // lanes per workgroup (k_emit): 8 waves share one copy of
-                                    // the tables (2 / 4 / 8 waves: emit 3.02 / 2.07 / 1.80 ms)
-#endif
-#define HH_NW (HH_NL / 64)          // waves per workgroup (k_emit)
+// k_emit's waves per workgroup share one copy of the tables: 16 (one
+// workgroup per CU with the 12-bit L1, 32 KiB) when the tables fit beside
+// them, else 8 (2 / 4 / 8 waves with the 11-bit L1: emit 3.02 / 2.07 / 1.80
+// ms; 16 with the 12-bit L1: 1.43 ms).
+#define HH_EMIT_NW_MAX 16
 #ifndef HH_FW
 #define HH_FW 4                     // waves per workgroup (k_front); 5 and 6 measured slower
                                     // (a 5-wave workgroup puts two waves on one SIMD)
@@ -290,9 +290,6 @@ __device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, 
 #ifndef HH_FRONT_MINB
 #define HH_FRONT_MINB 4   // workgroups per CU the front kernel's registers are sized for: with
                           // HH_FW = 5, 5 waves per SIMD (<= 96 VGPRs)
-#endif
-#ifndef HH_EMIT_MINW
-#define HH_EMIT_MINW 4
 #endif
 
 // Diagnostic build only (-DHH_DIAG): every wave stamps the shader clock
@@ -819,35 +816,36 @@ __device__ __forceinline__ void emit_run_direct(const hh_ctx *c, hh_cur cu, uint
 // k_front, a wave never waits for another: its tile's words, live lanes,
 // run offsets (a wave scan) and output staging are its own.
 // ---------------------------------------------------------------------------
-template <uint32_t SW>
-__global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__restrict__ gdata, Geometry geo,
+template <uint32_t SW, uint32_t NW>
+__global__ __launch_bounds__(64 * NW) void k_emit(const uint32_t *__restrict__ gdata, Geometry geo,
                                                                DevTab tab, Work wk, uint8_t *__restrict__ out,
                                                                uint64_t cap, uint64_t *dbg) {
     extern __shared__ __align__(16) uint8_t smem[];
-    __shared__ uint32_t s_eina[HH_NW][HH_NR];  // run entries pushed by walkers
-    __shared__ int16_t s_dina[HH_NW][HH_NR];   // their deltas
-    __shared__ uint8_t s_ka[HH_NW][HH_NR];
-    __shared__ uint8_t s_mema[HH_NW][HH_NR];
+    constexpr uint32_t NL = 64 * NW;
+    __shared__ uint16_t s_eina[NW][HH_NR];  // run entries pushed by walkers
+    __shared__ int16_t s_dina[NW][HH_NR];   // their deltas
+    __shared__ uint8_t s_ka[NW][HH_NR];
+    __shared__ uint8_t s_mema[NW][HH_NR];
 
     constexpr uint32_t S = 32 * SW;
     const uint32_t j = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     uint64_t *s_l1 = (uint64_t *)smem;                  // L1 entries as in global memory: one
                                                         // 64-bit read gives meta and symbols
     uint32_t *s_out = (uint32_t *)(s_l1 + HH_L1_SIZE) + wv * (HH_OBW / 4);   // the wave's staging
-    uint32_t *s_w = (uint32_t *)(s_l1 + HH_L1_SIZE) + HH_NW * (HH_OBW / 4) + wv * (SW * HH_NLS);
-    uint32_t *s_l2 = (uint32_t *)(s_l1 + HH_L1_SIZE) + HH_NW * (HH_OBW / 4 + SW * HH_NLS);
+    uint32_t *s_w = (uint32_t *)(s_l1 + HH_L1_SIZE) + NW * (HH_OBW / 4) + wv * (SW * HH_NLS);
+    uint32_t *s_l2 = (uint32_t *)(s_l1 + HH_L1_SIZE) + NW * (HH_OBW / 4 + SW * HH_NLS);
     uint32_t *s_tree = s_l2 + tab.l2_used;              // the compact tree (tail rule, long codes)
     uint8_t *s_tsym = (uint8_t *)(s_tree + tab.tree_lds);
-    uint32_t *s_ein = s_eina[wv];
+    uint16_t *s_ein = s_eina[wv];
     int16_t *s_din = s_dina[wv];
 
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
     const uint32_t span = HH_NCOL * S;
-    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += HH_NL) s_l1[i] = tab.l1[i];
-    for (uint32_t i = threadIdx.x; i < tab.l2_used; i += HH_NL) s_l2[i] = tab.l2[i];
+    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += NL) s_l1[i] = tab.l1[i];
+    for (uint32_t i = threadIdx.x; i < tab.l2_used; i += NL) s_l2[i] = tab.l2[i];
     // with the tree in LDS too, the decode loops issue no global load: a
     // global load there would make them wait for the next tile's prefetch
-    for (uint32_t i = threadIdx.x; i < tab.tree_lds; i += HH_NL) {
+    for (uint32_t i = threadIdx.x; i < tab.tree_lds; i += NL) {
         s_tree[i] = tab.tree[i];
         s_tsym[i] = tab.tsym[i];
     }
@@ -876,7 +874,7 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
     // block-local prefix), read out of those lanes where consumed.  Loads run
     // unconditionally, past the last tile on the last tile again.
     const uint64_t f0 = geo.emit_from;
-    const uint64_t nwv = (uint64_t)gridDim.x * HH_NW;
+    const uint64_t nwv = (uint64_t)gridDim.x * NW;
     const uint64_t tlast = geo.ntiles - 1;              // (launched only when f0 < ntiles)
     auto clampt = [&](uint64_t tt) { return tt < tlast ? tt : tlast; };
     Prefetch pf;
@@ -890,8 +888,8 @@ __global__ __launch_bounds__(HH_NL, HH_EMIT_MINW) void k_emit(const uint32_t *__
         meta_n = *src;
         prefetch_wtile<SW>(pf, gdata, tt * tile_bits / 32, geo.nwords);
     };
-    uint64_t t = f0 + (uint64_t)blockIdx.x * HH_NW + wv;
-    const uint32_t gwe = blockIdx.x * HH_NW + wv;       // this wave's list of deferred runs
+    uint64_t t = f0 + (uint64_t)blockIdx.x * NW + wv;
+    const uint32_t gwe = blockIdx.x * NW + wv;       // this wave's list of deferred runs
     uint32_t xqn = 0;
     if (t < geo.ntiles) prefetch_next(t);
     EDIAG_DECL
@@ -1308,11 +1306,14 @@ struct hh_decoder {
     uint32_t grid_f, grid_e, grid_w, grid_x;   // persistent grid sizes (occupancy x CUs)
     uint32_t fwalk;            // k_front's walk bound (HH_FRONT_WALK overrides)
     uint32_t ncu;              // compute units
+    uint32_t emit_nw;          // k_emit's waves per workgroup (size_grids)
+    uint32_t emit_nw_max;      // the largest tried (HH_EMIT_NW = 8 forces the smaller one)
     uint32_t xpt;              // k_emit's deferred runs per tile (HH_EMIT_XPT overrides)
     uint32_t grid_sw;          // words per region they were sized for
     size_t grid_l2;            // and the L2 table size
     uint32_t grid_tree;        // and the LDS tree size
     uint32_t grid_fdir;        // and the F escape directory
+    uint32_t grid_nw_max;      // and k_emit's largest workgroup
     // host staging of the evaluate() scope (hh_decode_host)
     uint8_t *h_stage;          // 2 x HH_HOST_CHUNK pinned (hh_decode_host)
     hipEvent_t h_ev[2];
@@ -1442,6 +1443,9 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     const char *fw = getenv("HH_FRONT_WALK");            // experiments, tests
     if (fw && *fw) d->fwalk = (uint32_t)atoi(fw);
     d->xpt = HH_XPT;
+    d->emit_nw_max = HH_EMIT_NW_MAX;
+    const char *enw = getenv("HH_EMIT_NW");
+    if (enw && atoi(enw) == 8) d->emit_nw_max = 8;
     const char *xp = getenv("HH_EMIT_XPT");
     if (xp && *xp) d->xpt = (uint32_t)atoi(xp);
     d->G = hh_pick_overlap(d->ht);
@@ -1482,8 +1486,8 @@ static size_t lds_walk(uint32_t sw, uint32_t l2, uint32_t fdir) {
 static size_t lds_emitx(uint32_t sw, uint32_t l2) {
     return (size_t)HH_L1_SIZE * 8 + (size_t)((l2 + 3) & ~3u) * 4 + (size_t)((HH_KM + 1) * sw + 6) * 64 * 4;
 }
-static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree) {
-    return (2 * (size_t)HH_L1_SIZE + (size_t)HH_NW * sw * HH_NLS + l2) * 4 + (size_t)HH_NW * HH_OBW +
+static size_t lds_emit(uint32_t sw, uint32_t l2, uint32_t tree, uint32_t nw) {
+    return (2 * (size_t)HH_L1_SIZE + (size_t)nw * sw * HH_NLS + l2) * 4 + (size_t)nw * HH_OBW +
            (size_t)tree * 5;
 }
 
@@ -1515,9 +1519,9 @@ static kemitx_t kemitx_for(uint32_t sw) {
     default: return nullptr;
     }
 }
-static kemit_t kemit_for(uint32_t sw) {
+static kemit_t kemit_for(uint32_t sw, uint32_t nw) {
     switch (sw) {
-#define X(n) case n: return k_emit<n>;
+#define X(n) case n: return nw == 16 ? k_emit<n, 16> : k_emit<n, 8>;
         HH_SW_CASES(X)
 #undef X
     default: return nullptr;
@@ -1527,13 +1531,21 @@ static kemit_t kemit_for(uint32_t sw) {
 // Persistent grids: the occupancy answer x CUs for each kernel.
 static int size_grids(hh_decoder *d, uint32_t sw) {
     if (d->grid_f && d->grid_sw == sw && d->grid_l2 == d->tab.l2_used && d->grid_tree == d->tab.tree_lds &&
-        d->grid_fdir == d->tab.fdir_used)
+        d->grid_fdir == d->tab.fdir_used && d->grid_nw_max == d->emit_nw_max)
         return HH_OK;
     int pf = 0, pe = 0, pw = 0, px = 0, ncu = 0;
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pf, kfront_for(sw), 64 * HH_FW, lds_front(sw, d->tab.l2_used, d->tab.fdir_used)));
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pw, kwalk_for(sw), HH_WALK_T, lds_walk(sw, d->tab.l2_used, d->tab.fdir_used)));
     HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&px, kemitx_for(sw), 64, lds_emitx(sw, d->tab.l2_used)));
-    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kemit_for(sw), HH_NL, lds_emit(sw, d->tab.l2_used, d->tab.tree_lds)));
+    uint32_t nw = d->emit_nw_max;
+    for (;; nw /= 2) {
+        pe = 0;
+        const size_t lds = lds_emit(sw, d->tab.l2_used, d->tab.tree_lds, nw);
+        if (lds + (size_t)nw * HH_NR * 6 <= 160 * 1024)   // (+ the static per-wave arrays)
+            HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kemit_for(sw, nw), 64 * nw, lds));
+        if (pe >= 1 || nw == 8) break;
+    }
+    d->emit_nw = nw;
     HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, d->device));
     if (pf < 1 || pe < 1 || pw < 1 || px < 1) return HH_ERR_UNSUPPORTED;
     d->grid_f = (uint32_t)(pf * ncu);
@@ -1545,6 +1557,7 @@ static int size_grids(hh_decoder *d, uint32_t sw) {
     d->grid_l2 = d->tab.l2_used;
     d->grid_tree = d->tab.tree_lds;
     d->grid_fdir = d->tab.fdir_used;
+    d->grid_nw_max = d->emit_nw_max;
     return HH_OK;
 }
 
@@ -1638,9 +1651,10 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     const size_t o_qn = o_blk + (size_t)nblk * 8, o_q = (o_qn + (size_t)geo.nfw * 4 + 7) & ~(size_t)7;
     const size_t o_xn = o_q + (size_t)geo.nfw * geo.qcap * 8;
     const uint64_t ne = nt > emit_from ? nt - emit_from : 0;
-    const uint64_t ng = (ne + HH_NW - 1) / HH_NW;          // workgroups' worth of tiles
+    const uint32_t enw = d->emit_nw;
+    const uint64_t ng = (ne + enw - 1) / enw;              // workgroups' worth of tiles
     const uint32_t ge = (uint32_t)(ng < d->grid_e ? (ng ? ng : 1) : d->grid_e);
-    const uint32_t nwe = ge * HH_NW;                        // k_emit's waves
+    const uint32_t nwe = ge * enw;                          // k_emit's waves
     geo.xcap = (uint32_t)((ne + nwe - 1) / nwe * d->xpt);
     const size_t o_xqn = o_xn + (nt + 1) * HH_NR * 4, o_xq = (o_xqn + (size_t)nwe * 4 + 15) & ~(size_t)15;
     const size_t need = o_xq + (size_t)nwe * geo.xcap * 16;
@@ -1661,12 +1675,12 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     wk.xq = (uint64_t *)(w + o_xq);
     const kfront_t kf = kfront_for(geo.sw);
     const kwalk_t kw = kwalk_for(geo.sw);
-    const kemit_t ke = kemit_for(geo.sw);
+    const kemit_t ke = kemit_for(geo.sw, enw);
     const kemitx_t kx = kemitx_for(geo.sw);
     if (!kf || !kw || !ke || !kx) return HH_ERR_UNSUPPORTED;
     // k_emit, then the runs it deferred
     auto launch_emit = [&]() -> int {
-        hipLaunchKernelGGL(ke, dim3(ge), dim3(HH_NL), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds), st,
+        hipLaunchKernelGGL(ke, dim3(ge), dim3(64 * enw), lds_emit(geo.sw, d->tab.l2_used, d->tab.tree_lds, enw), st,
                            (const uint32_t *)d_data, geo, d->tab, wk, (uint8_t *)d_out, cap, d->d_dbg);
         HIP_OK(hipGetLastError());
         hipLaunchKernelGGL(kx, dim3(d->grid_x), dim3(64), lds_emitx(geo.sw, d->tab.l2_used), st,

@@ -12,7 +12,8 @@
  *     bits 32..36  nbits: total code bits of the nsym complete symbols
  *     bits 37..39  nsym:  0 = escape (first code longer than HH_P bits)
  *     bits 40..44  len0:  code length of the first symbol (nsym > 0)
- *     bits 45..55  bmask: start offsets of the nsym symbols (bit 0 = first)
+ *     bits 45..    bmask: start offsets of the nsym symbols (bit 0 = first),
+ *                  HH_P bits
  *     escape entries (nsym == 0):
  *     bits  0..15  L2 base index of the subtable for the depth-HH_P node
  *     bits 16..20  q: index bits of that subtable (<= HH_Q_MAX)
@@ -52,7 +53,8 @@
 #include <stdint.h>
 
 #ifndef HH_P
-#define HH_P 11                 /* L1 index bits                      */
+#define HH_P 12                 /* L1 index bits (11: k_emit 17 % slower on
+                                   kjv, with half the table in LDS)    */
 #endif
 #define HH_L1_SIZE (1u << HH_P)
 #ifndef HH_PF
@@ -67,7 +69,7 @@
 #define HH_L1_NBITS(e) ((uint32_t)((e) >> 32) & 31u)
 #define HH_L1_NSYM(e) ((uint32_t)((e) >> 37) & 7u)
 #define HH_L1_LEN0(e) ((uint32_t)((e) >> 40) & 31u)
-#define HH_L1_BMASK(e) ((uint32_t)((e) >> 45) & 0x7ffu)
+#define HH_L1_BMASK(e) ((uint32_t)((e) >> 45) & ((1u << HH_P) - 1u))
 #define HH_L1_SYMS(e) ((uint32_t)(e))
 #define HH_L1_L2BASE(e) ((uint32_t)(e) & 0xffffu)
 #define HH_L1_L2Q(e) (((uint32_t)(e) >> 16) & 31u)
