@@ -466,8 +466,7 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
 // comparisons (hh_walk_exits, restated here region by region) against the
 // regions' pass-1 exits and counts (xn).  A lane stages only the words of
 // the region it walks (from G bits before it, for the heads of regions that
-// were not decoded, to a halo past it) at LDS index (q * HH_WALK_T + lane),
-// double-buffered: region k+1's words are loaded while region k is walked.
+// were not decoded, to a halo past it) at LDS index (q * HH_WALK_T + lane).
 // The lane's record replaces k_front's placeholder.
 // ---------------------------------------------------------------------------
 #define HH_WALK_T 256
@@ -494,7 +493,7 @@ __global__ __launch_bounds__(HH_WALK_T) void k_walk(const uint32_t *__restrict__
     uint16_t *s_f = (uint16_t *)smem;                   // F, its escape directory, L2
     uint32_t *s_fdir = (uint32_t *)smem + HH_F_SIZE / 2;
     uint32_t *s_l2 = s_fdir + ((tab.fdir_used + 3u) & ~3u);
-    uint32_t *s_win = (uint32_t *)smem + ftab_words(tab.fdir_used, tab.l2_used) + tid;   // 2 x NW words
+    uint32_t *s_win = (uint32_t *)smem + ftab_words(tab.fdir_used, tab.l2_used) + tid;   // NW words
     load_ftables(tab, s_f, s_fdir, s_l2);
     __syncthreads();
     const uint64_t tile_bits = (uint64_t)HH_NR * S;
@@ -555,11 +554,14 @@ __global__ __launch_bounds__(HH_WALK_T) void k_walk(const uint32_t *__restrict__
         A = A < bt ? A : bt;
         hh_wk w = {0u, 0u, 0u, 0, 0u, 0u};
         for (uint32_t k = 1; k <= HH_KM; k++) {
-            const uint32_t sl = (k & 1u) * NW, g0 = win0(k);
+            const uint32_t g0 = win0(k);
+            // (most walks end in their first region: the next region's words
+            // are loaded only when the walk goes on -- loading them ahead
+            // doubled k_walk's HBM reads)
+            if (k > 1) walk_win_load<SW>(pre, gdata, tw0 + g0, geo.nwords);
 #pragma unroll
-            for (uint32_t q = 0; q < NW; q++) s_win[(sl + q) * HH_WALK_T] = pre[q];
-            if (k < HH_KM) walk_win_load<SW>(pre, gdata, tw0 + win0(k + 1), geo.nwords);
-            c.w = s_win + ((int32_t)sl - (int32_t)g0) * (int32_t)HH_WALK_T;   // tile word g at (sl + g - g0)
+            for (uint32_t q = 0; q < NW; q++) s_win[q * HH_WALK_T] = pre[q];
+            c.w = s_win - (int32_t)g0 * (int32_t)HH_WALK_T;                  // tile word g at (g - g0)
             const uint32_t rg = j + k, R = rg * S;
             const uint32_t Ec = R + S < bt ? R + S : bt;
             // the region's own chain: its pass-1 exit and count (a tile past
@@ -1481,7 +1483,7 @@ static size_t lds_front(uint32_t sw, uint32_t l2, uint32_t fdir) {
 }
 static uint32_t walk_win(uint32_t sw) { return sw + 6; }   // WalkWin<sw>::n
 static size_t lds_walk(uint32_t sw, uint32_t l2, uint32_t fdir) {
-    return ((size_t)ftab_words(fdir, l2) + (size_t)2 * walk_win(sw) * HH_WALK_T) * 4;
+    return ((size_t)ftab_words(fdir, l2) + (size_t)walk_win(sw) * HH_WALK_T) * 4;
 }
 static size_t lds_emitx(uint32_t sw, uint32_t l2) {
     return (size_t)HH_L1_SIZE * 8 + (size_t)((l2 + 3) & ~3u) * 4 + (size_t)((HH_KM + 1) * sw + 6) * 64 * 4;
