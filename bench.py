@@ -5,8 +5,9 @@ Workload (BASELINE.json configs[2]): a synthetic 1 GiB English-text .huff --
 kjv.txt tiled (about 349.4 copies) and encoded with the files/kjv.txt.huff
 codebook, cut at a symbol boundary -- decoded on each MI355X.  One "step" is
 one full decode of that stream with the input already resident in HBM:
-hh_decode_device (k_front: overlap heads, speculative region decode, walks,
-transfer tables; k_scan1/k_scan2: entering states and tile bases; k_emit:
+hh_decode_device (k_front: overlap heads, speculative region decode, exit
+merges; k_walk: the deferred walks; k_table: transfer tables;
+k_scan1/k_scan2: entering states and tile bases; k_emit + k_emitx:
 emission) plus its status readback.  For N > 1 the stream is N GiB, sharded
 by whole tiles (weak scaling); each step is the rank's segment decode (with
 its prologue tiles) plus the entry-state exchange (one 5-integer

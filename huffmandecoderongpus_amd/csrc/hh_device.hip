@@ -762,6 +762,19 @@ __global__ __launch_bounds__(1024) void k_scan2(Geometry geo, Work wk, uint32_t 
 }
 
 // ---------------------------------------------------------------------------
+// The emission loops take whole L1 lookups while p < this bound, then one
+// lookup or symbol at a time.  A run's symbols all end by its end pe (a
+// boundary of the true chain): a lookup from p < pe - HH_P ends by pe, and so
+// does an escape's single symbol.  Only the stream's last run, which may end
+// in a code cut by the end of the stream (the tail rule), keeps the longest
+// code's margin.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t whole_lookups_end(uint32_t pe, uint32_t bt, uint32_t maxadv) {
+    const uint32_t m = pe < bt ? HH_P : maxadv;
+    return pe > m ? pe - m : 0u;
+}
+
+// ---------------------------------------------------------------------------
 // A run [cu.p, pe) of the true chain decoded straight to HBM at dst: bytes up
 // to a dword boundary, then dwords, then the ragged end (the first and last
 // dwords may be shared with the neighbouring runs).
@@ -777,8 +790,7 @@ __device__ __forceinline__ void emit_run_direct(const hh_ctx *c, hh_cur cu, uint
     }
     uint64_t acc = 0;
     uint32_t nacc = 0;
-    // whole lookups while the longest possible one still ends by pe
-    const uint32_t pf_end = pe > maxadv ? pe - maxadv : 0u;
+    const uint32_t pf_end = whole_lookups_end(pe, c->bt, maxadv);
     while (cu.p < pf_end) {
         const uint32_t win = hh_cur_win(cu);
         const uint64_t le = c->l1[win & (HH_L1_SIZE - 1u)];
@@ -970,9 +982,9 @@ __global__ __launch_bounds__(64 * NW) void k_emit(const uint32_t *__restrict__ g
             EDIAG_STAMP(1);                             // (zeroing)
             if (cu.p < pe) {
                 const uint32_t b = a0 + L;
-                uint32_t wd = b >> 2, nacc = b & 3u, emitted = 0, val, k;
+                uint32_t wd = b >> 2, nacc = b & 3u, val, k;
                 uint64_t acc = 0;
-                const uint32_t pf_end = pe > geo.maxadv ? pe - geo.maxadv : 0u;
+                const uint32_t pf_end = whole_lookups_end(pe, bt, geo.maxadv);
                 while (cu.p < pf_end) {            // whole lookups
                     const uint32_t win = hh_cur_win(cu);
                     const uint32_t ix = win & (HH_L1_SIZE - 1u);
@@ -985,24 +997,15 @@ __global__ __launch_bounds__(64 * NW) void k_emit(const uint32_t *__restrict__ g
                     }
                     acc |= (uint64_t)sy << (8 * nacc);
                     nacc += ns;
-                    emitted += ns;
-#ifdef HH_EXP_ORALL
-                    // every step ORs the open dword (idempotent), no branch
-                    atomicOr(&s_out[wd], (uint32_t)acc);
-                    const bool full = nacc >= 4;
-                    wd += full ? 1u : 0u;
-                    acc = full ? acc >> 32 : acc;
-                    nacc -= full ? 4u : 0u;
-#else
                     if (nacc >= 4) {
                         atomicOr(&s_out[wd], (uint32_t)acc);
                         wd++;
                         acc >>= 32;
                         nacc -= 4;
                     }
-#endif
                     hh_cur_adv(&c, cu, nb);
                 }
+                uint32_t emitted = 4 * wd + nacc - b;
                 while (cu.p < pe) {                // the end of the run (and of the stream)
                     hh_emit_step(&c, cu, pe, emitted, rc, &val, &k);
                     acc |= (uint64_t)val << (8 * nacc);

@@ -1,4 +1,4 @@
-"""A/B timing (tools/ab.sh): the decode pipeline on the synthetic stream with
+"""A/B timing (tools/gpu_walkab.sh, tools/gpu_envab.sh): the decode pipeline on the synthetic stream with
 the library named by HIPHUFF_LIB (default: the in-tree build); prints one
 JSON line with the median device time of each kernel phase over N runs and
 whether the output matched the tiled text.
@@ -19,7 +19,7 @@ from huffmandecoderongpus_amd import synth  # noqa: E402
 mib = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 src = sys.argv[3] if len(sys.argv) > 3 else "kjv.txt"
-# the source text comes from the in-tree library (tools/ab.sh caches it), so
+# the source text comes from the in-tree library (the A/B scripts cache it), so
 # that an experiment variant under test never decodes its own reference
 cache = os.environ.get("HH_TEXT_CACHE")
 if cache and os.path.exists(cache):
