@@ -322,8 +322,11 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
      * costs no address arithmetic.  (mlo, mhi) accumulate words p>>5 and
      * p>>5 + 1; the region starts word-aligned. */
     uint32_t mlo = 0, mhi = 0;
-    /* main loop: every symbol of a step starts before lim */
-    const uint32_t lf = lim > c->maxadv ? lim - c->maxadv : 0u;
+    /* main loop: every symbol of a step starts before lim -- a lookup's
+     * symbols start within its index bits, an escape's one symbol at p (its
+     * code may run past lim, or be cut by the end of the stream: hh_escape) */
+    const uint32_t pidx = c->pf ? c->pf : HH_P;
+    const uint32_t lf = lim > pidx ? lim - pidx : 0u;
     while (u.p < lf) {
         const uint32_t win = hh_cur_win(u);
         uint32_t ns, nb, bm;
