@@ -469,7 +469,9 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
 // were not decoded, to a halo past it) at LDS index (q * HH_WALK_T + lane).
 // The lane's record replaces k_front's placeholder.
 // ---------------------------------------------------------------------------
-#define HH_WALK_T 256
+#ifndef HH_WALK_T
+#define HH_WALK_T 256   // lanes per k_walk workgroup (64: +0.05 ms; 512: same)
+#endif
 template <uint32_t SW>
 struct WalkWin {
     static constexpr uint32_t n = SW + 6;   // words of one region's window

@@ -33,7 +33,7 @@ else:
         np.save(cache, text)
         sys.exit(0)
 syn = synth.tiled_stream(hf, text, mib << 20)
-dec = H.Decoder(0, flags=int(os.environ.get("HH_FLAGS", "0")))
+dec = H.Decoder(0, lane_bits=int(os.environ.get("HH_LANE_BITS", "0")), flags=int(os.environ.get("HH_FLAGS", "0")))
 dec.set_tree(syn.tree)
 out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device="cuda")
 ph = {"total": [], "sync": [], "scan": [], "emit": []}
