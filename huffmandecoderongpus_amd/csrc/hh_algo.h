@@ -392,7 +392,9 @@ HH_HD uint32_t hh_region_count(const hh_ctx *c, uint32_t p0, uint32_t lim, uint3
  * [s, R) as bits of *head (bit i <=> a symbol starts at s + i).  Pass 1 then
  * counts C_r from y, exactly as a chain started at y (so counts, masks and
  * walks keep the offset-0 semantics with R's entry point y instead of R). */
-#define HH_GMAX 64u           /* largest overlap */
+#ifndef HH_GMAX
+#define HH_GMAX 64u           /* largest overlap (k_walk stages G bits before a region) */
+#endif
 HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, uint64_t *head) {
     uint64_t h = 0;
     hh_cur u = hh_cur_at(c, s);

@@ -104,7 +104,6 @@ struct Geometry {
     uint64_t nwords;     // readable payload words
     uint64_t ntiles;
     uint32_t S, sw;
-    uint32_t vec4;       // 16-B aligned payload and sw % 4 == 0
     uint32_t maxadv;     // max(HH_P, longest code)
     uint32_t G;          // overlap bits (hh_region_head)
     uint32_t in_state;   // state entering tile 0 (a shard's entry; 0 at the stream start)
@@ -277,19 +276,9 @@ __host__ __device__ constexpr uint32_t ftab_words(uint32_t fdir, uint32_t l2) {
     return HH_F_SIZE / 2 + ((fdir + 3u) & ~3u) + ((l2 + 3u) & ~3u);
 }
 
-// Decode tables into LDS (meta halves always; symbol halves when s_l1s).
-__device__ __forceinline__ void load_tables(const DevTab &tab, uint32_t *s_l1m, uint32_t *s_l1s, uint32_t *s_l2) {
-    for (uint32_t i = threadIdx.x; i < HH_L1_SIZE; i += blockDim.x) {
-        const uint64_t e = tab.l1[i];
-        s_l1m[i] = (uint32_t)(e >> 32);
-        if (s_l1s) s_l1s[i] = (uint32_t)e;
-    }
-    for (uint32_t i = threadIdx.x; i < tab.l2_used; i += blockDim.x) s_l2[i] = tab.l2[i];
-}
-
 #ifndef HH_FRONT_MINB
-#define HH_FRONT_MINB 4   // workgroups per CU the front kernel's registers are sized for: with
-                          // HH_FW = 5, 5 waves per SIMD (<= 96 VGPRs)
+#define HH_FRONT_MINB 4   // workgroups per CU the front kernel's registers are sized for (it
+                          // compiles to ~68 VGPRs: 7 waves per SIMD, as many as its LDS allows)
 #endif
 
 // Diagnostic build only (-DHH_DIAG): every wave stamps the shader clock
@@ -1029,11 +1018,7 @@ __global__ __launch_bounds__(64 * NW) void k_emit(const uint32_t *__restrict__ g
             for (uint32_t i = j; i < nq; i += 64) {
                 const uint32_t lo = 16 * i;
                 if (lo >= a0 && lo + 16 <= a0 + Tout) {
-#ifndef HH_EXP_PLAIN_STORE
                     __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
-#else
-                    *(u32x4 *)(gb + lo) = *(const u32x4 *)(sb + lo);
-#endif
                 } else {                           // a block shared with a neighbouring tile
                     const uint32_t e = lo + 16 < a0 + Tout ? lo + 16 : a0 + Tout;
                     for (uint32_t q = lo > a0 ? lo : a0; q < e; q++) gb[q] = sb[q];
@@ -1642,7 +1627,6 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     const uint64_t tb = (uint64_t)HH_NR * d->S;
     const uint64_t all = (bits_avail + tb - 1) / tb;
     geo.ntiles = ntiles && ntiles < all ? ntiles : all;
-    geo.vec4 = (((uintptr_t)d_data & 15u) == 0) && (geo.sw % 4 == 0);
     const uint64_t nt = geo.ntiles;
     const uint32_t nblk = (uint32_t)((nt + 1 + HH_SCAN_TB - 1) / HH_SCAN_TB);
     // workspace: flags 64 B | tabs | recs | st | lex | blk | q
