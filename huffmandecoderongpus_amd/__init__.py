@@ -63,7 +63,7 @@ class _Config(C.Structure):
 class _Stats(C.Structure):
     _fields_ = [("ms_total", C.c_double), ("ms_sync", C.c_double), ("ms_scan", C.c_double),
                 ("ms_emit", C.c_double), ("out_len", C.c_uint64), ("lanes", C.c_uint64),
-                ("repairs", C.c_uint64), ("exact_fallback", C.c_int)]
+                ("repairs", C.c_uint64), ("exact_fallback", C.c_int), ("fixed_length", C.c_int)]
 
 
 class _Range(C.Structure):

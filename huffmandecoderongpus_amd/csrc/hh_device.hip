@@ -1099,6 +1099,74 @@ __global__ __launch_bounds__(64) void k_emitx(const uint32_t *__restrict__ gdata
 }
 
 // ---------------------------------------------------------------------------
+// k_fixed: a complete fixed-length code (2^L symbols, every code L <= 8
+// bits) needs no chain: symbol i is the L bits at i * L.  One thread per 16
+// symbols, a 16-B store each; the stream's last code, if the end cuts it,
+// takes the reference's tail rule (the node its bits reach,
+// decodeallbits.cl:20-31).  sym[w] is the symbol of the L-bit window w
+// (stream bit p in bit 0).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fixed(const uint32_t *__restrict__ gdata, uint64_t bits, uint32_t L,
+                                               const uint8_t *__restrict__ fsym, DevTab tab,
+                                               uint8_t *__restrict__ out, uint64_t nsym) {
+    __shared__ uint8_t s_sym[256];
+    __shared__ uint32_t s_b4[256];                      // L = 2: a byte's four symbols
+    const bool a16 = ((uintptr_t)out & 15u) == 0;
+    s_sym[threadIdx.x] = fsym[threadIdx.x];
+    {
+        const uint32_t b = threadIdx.x;
+        s_b4[b] = fsym[b & 3u] | (uint32_t)fsym[(b >> 2) & 3u] << 8 | (uint32_t)fsym[(b >> 4) & 3u] << 16 |
+                  (uint32_t)fsym[b >> 6] << 24;
+    }
+    __syncthreads();
+    const uint64_t nfull = bits / L;                    // whole codes
+    const uint32_t mask = (1u << L) - 1u;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g * 16 < nsym;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i0 = g * 16, p0 = i0 * L;
+        if (L == 2 && i0 + 16 <= nfull && a16) {       // (E.coli) one word, four byte lookups
+            const uint32_t w = gdata[g];
+            *(u32x4 *)(out + i0) = (u32x4){s_b4[w & 255u], s_b4[(w >> 8) & 255u], s_b4[(w >> 16) & 255u],
+                                           s_b4[w >> 24]};
+            continue;
+        }
+        uint64_t wi = p0 >> 5;
+        uint64_t buf = ((uint64_t)gdata[wi + 1] << 32 | gdata[wi]) >> (p0 & 31);
+        uint32_t have = 64 - (uint32_t)(p0 & 31);
+        wi += 2;
+        uint32_t v[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t k = 0; k < 16; k++) {
+            if (have < L) {                             // (L <= 8: one word tops it up)
+                buf |= (uint64_t)gdata[wi++] << have;
+                have += 32;
+            }
+            v[k >> 2] |= (uint32_t)s_sym[(uint32_t)buf & mask] << (8 * (k & 3));
+            buf >>= L;
+            have -= L;
+        }
+        if (i0 + 16 <= nfull && a16) {
+            *(u32x4 *)(out + i0) = (u32x4){v[0], v[1], v[2], v[3]};
+        } else {                                        // the stream's end (or an unaligned output)
+            for (uint32_t k = 0; k < 16 && i0 + k < nsym; k++) {
+                uint8_t b = (uint8_t)(v[k >> 2] >> (8 * (k & 3)));
+                if (i0 + k == nfull) {                  // a code cut by the end: the tail rule
+                    uint32_t node = 0;
+                    for (uint64_t p = nfull * L; p < bits; p++) {
+                        const uint32_t tn = tab.tree[node];
+                        if (tn & HH_T_LEAF) break;
+                        const uint32_t bit = (gdata[p >> 5] >> (p & 31)) & 1u;
+                        node = bit ? (tn >> 15) & 0x7fffu : tn & 0x7fffu;
+                    }
+                    b = tab.tsym[node];
+                }
+                out[i0 + k] = b;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Segment path: exact and O(N) for any code of at most 32 bits, whether or
 // not it resynchronises (the fast path's walks need it to).  The stream is
 // cut into segments of `seglen` bits.  The chain through a segment is fixed
@@ -1298,6 +1366,8 @@ struct hh_decoder {
     uint32_t grid_f, grid_e, grid_w, grid_x;   // persistent grid sizes (occupancy x CUs)
     uint32_t fwalk;            // k_front's walk bound (HH_FRONT_WALK overrides)
     uint32_t ncu;              // compute units
+    uint32_t fixed_len;        // L of a complete fixed-length code (k_fixed), else 0
+    uint8_t *d_fsym;           // its 256-entry window -> symbol table
     uint32_t emit_nw;          // k_emit's waves per workgroup (size_grids)
     uint32_t emit_nw_max;      // the largest tried (HH_EMIT_NW = 8 forces the smaller one)
     uint32_t xpt;              // k_emit's deferred runs per tile (HH_EMIT_XPT overrides)
@@ -1344,6 +1414,7 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
         hipMalloc(&d->d_l2, sizeof(uint32_t) * HH_L2_MAX) != hipSuccess ||
         hipMalloc(&d->d_f, sizeof(uint16_t) * HH_F_SIZE) != hipSuccess ||
         hipMalloc(&d->d_fdir, sizeof(uint32_t) * HH_L2_MAX) != hipSuccess ||
+        hipMalloc(&d->d_fsym, 256) != hipSuccess ||
         hipMalloc(&d->d_tree, sizeof(uint32_t) * (HH_TREE_MAX + 1)) != hipSuccess ||
         hipMalloc(&d->d_tsym, HH_TREE_MAX + 1) != hipSuccess ||
         hipMalloc(&d->d_max, 16) != hipSuccess ||
@@ -1370,6 +1441,7 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
     if (d->d_l2) hipFree(d->d_l2);
     if (d->d_f) hipFree(d->d_f);
     if (d->d_fdir) hipFree(d->d_fdir);
+    if (d->d_fsym) hipFree(d->d_fsym);
     if (d->d_tree) hipFree(d->d_tree);
     if (d->d_tsym) hipFree(d->d_tsym);
     if (d->d_max) hipFree(d->d_max);
@@ -1431,6 +1503,22 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     d->tab.l2_used = d->ht->l2_used;
     d->tab.tree_lds = d->ht->tree_used;
     d->S = pick_region_bits(d->ht, d->cfg.lane_bits);
+    // a complete fixed-length code: every L-bit window is one symbol
+    d->fixed_len = 0;
+    const int L = d->ht->fixed_len;
+    if (L >= 1 && L <= 8 && d->ht->tree_used == (2u << L) - 1u) {
+        uint8_t fs[256];
+        for (uint32_t w = 0; w < 256; w++) {
+            uint32_t node = 0;
+            for (int b = 0; b < L; b++) {
+                const uint32_t tn = d->ht->tree[node];
+                node = (w >> b) & 1u ? (tn >> 15) & 0x7fffu : tn & 0x7fffu;
+            }
+            fs[w] = (uint8_t)(d->ht->tree[node] & 0xffu);
+        }
+        HIP_OK(hipMemcpy(d->d_fsym, fs, 256, hipMemcpyHostToDevice));
+        d->fixed_len = (uint32_t)L;
+    }
     d->fwalk = HH_FRONT_WALK;
     const char *fw = getenv("HH_FRONT_WALK");            // experiments, tests
     if (fw && *fw) d->fwalk = (uint32_t)atoi(fw);
@@ -1801,6 +1889,31 @@ out:
     return rc;
 }
 
+// A complete fixed-length code: k_fixed (above).
+static int fixed_path(hh_decoder *d, const void *d_data, uint64_t bits, uint8_t *d_out, uint64_t cap,
+                      uint64_t *out_len, hipStream_t st) {
+    const uint32_t L = d->fixed_len;
+    const uint64_t nsym = bits / L + (bits % L ? 1 : 0);
+    *out_len = nsym;
+    d->stats.out_len = nsym;
+    d->stats.fixed_length = 1;
+    if (nsym > cap) return HH_ERR_CAPACITY;
+    const uint64_t nthr = (nsym + 15) / 16, cap_blk = (uint64_t)(d->ncu ? d->ncu : 256) * 32;
+    uint64_t nb = (nthr + 255) / 256;
+    if (nb > cap_blk) nb = cap_blk;
+    HIP_OK(hipEventRecord(d->ev[0], st));
+    hipLaunchKernelGGL(k_fixed, dim3((unsigned)nb), dim3(256), 0, st, (const uint32_t *)d_data, bits, L,
+                       (const uint8_t *)d->d_fsym, d->tab, d_out, nsym);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipEventRecord(d->ev[3], st));
+    HIP_OK(hipStreamSynchronize(st));
+    float ms = 0;
+    hipEventElapsedTime(&ms, d->ev[0], d->ev[3]);
+    d->stats.ms_emit = ms;
+    d->stats.ms_total = ms;
+    return HH_OK;
+}
+
 extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits, void *d_out,
                                 uint64_t cap, uint64_t *out_len, void *hip_stream) {
     if (!d || !out_len || (!d_data && bits) || (!d_out && cap)) return HH_ERR_ARG;
@@ -1813,6 +1926,8 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     memset(&d->stats, 0, sizeof(d->stats));
     *out_len = 0;
     if (bits == 0) return HH_OK;
+    if (d->fixed_len && !(d->cfg.flags & (HH_FLAG_NO_FIXED | HH_FLAG_FORCE_EXACT | HH_FLAG_FORCE_SEGMENT)))
+        return fixed_path(d, d_data, bits, (uint8_t *)d_out, cap, out_len, st);
     const bool seg_ok = d->ht->maxlen <= HH_MAXLEN_FAST && !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
     if (!fast_path_ok(d) || (d->cfg.flags & HH_FLAG_FORCE_SEGMENT)) {
         if (seg_ok) {

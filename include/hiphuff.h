@@ -133,6 +133,10 @@ typedef struct {
                                    segment path (exact, O(N), any length;
                                    the path codes that do not resynchronise
                                    take, codes <= 32 bits) */
+#define HH_FLAG_NO_FIXED 4      /* a complete fixed-length code (2^L symbols,
+                                   every code L <= 8 bits, e.g. E.coli's) is
+                                   unpacked directly (k_fixed) unless this is
+                                   set: then it takes the general pipeline */
 
 int hh_decoder_create(hh_decoder **dec, const hh_config *cfg);
 void hh_decoder_destroy(hh_decoder *dec);
@@ -156,6 +160,8 @@ typedef struct {
                                 pipeline (codes longer than 32 bits); 2: the
                                 segment path (a walk found no merge: a code
                                 that does not resynchronise)                */
+    int fixed_length;        /* 1: a complete fixed-length code, unpacked
+                                by k_fixed (HH_FLAG_NO_FIXED: 0)            */
 } hh_stats;
 
 int hh_decoder_stats(const hh_decoder *dec, hh_stats *st);

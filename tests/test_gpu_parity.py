@@ -164,6 +164,50 @@ def test_multi_region_walks_and_transfer_tables(hh):
         dec.close()
 
 
+@pytest.mark.parametrize("depth", range(1, 9))
+def test_fixed_length_codes_unpacked(hh, depth):
+    """Complete fixed-length codes (2^L symbols of L bits: E.coli's shape)
+    are unpacked by k_fixed; streams cut inside a code take the tail rule.
+    Both paths -- k_fixed and the general pipeline (HH_FLAG_NO_FIXED = 4) --
+    against the oracle, on an unaligned output too."""
+    import torch
+    rng = np.random.default_rng(depth)
+    iz, io, sy = _complete_tree(depth)
+    sy = sy.copy()
+    sy[iz >= 0] = rng.integers(0, 256, int((iz >= 0).sum()))   # internal nodes: tail-rule bytes
+    tree = hh.Tree(iz, io, sy)
+    for bits in (1, depth, 16 * depth + 1, 100003, (1 << 20) * depth + depth - 1):
+        data = rng.integers(0, 256, (bits + 7) // 8 + 8, dtype=np.uint8)
+        want = _oracle(iz, io, sy, data, bits)
+        for flags in (0, 4):
+            dec = hh.Decoder(0, flags=flags)
+            try:
+                dec.set_tree(tree)
+                got = _decode_dev(hh, dec, data, bits, len(want) + 16)
+                assert dec.stats()["fixed_length"] == (1 if flags == 0 else 0)
+            finally:
+                dec.close()
+            assert len(got) == len(want) and np.array_equal(got, want), (depth, bits, flags)
+    # an output pointer off 16-B alignment
+    bits = 4096 * depth + 1
+    data = rng.integers(0, 256, (bits + 7) // 8 + 8, dtype=np.uint8)
+    want = _oracle(iz, io, sy, data, bits)
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(tree)
+        buf = np.zeros((bits + 7) // 8 + 64, np.uint8)
+        buf[: (bits + 7) // 8] = data[: (bits + 7) // 8]
+        d_in = torch.from_numpy(buf).cuda()
+        d_out = torch.zeros(len(want) + 64, dtype=torch.uint8, device="cuda")
+        n = dec.decode_device(d_in, bits, d_out[3:])
+        torch.cuda.synchronize()
+        got = d_out.cpu().numpy()
+        assert n == len(want) and np.array_equal(got[3:3 + n], want)
+        assert not got[:3].any() and not got[3 + n:].any()
+    finally:
+        dec.close()
+
+
 def test_capacity_error(hh, files_dir):
     path = os.path.join(files_dir, "paper1.huff")
     hf = hh.HuffFile.load(path)
