@@ -132,7 +132,8 @@ def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, s
             "ms_emit": round(statistics.mean(s["ms_emit"] for s in st), 4),
             "compressed_bytes": C, "decoded_bytes": n_want,
             "roofline_frac": round(ach / HBM_PEAK_GBS, 4),
-            "fast_path": all(s["exact_fallback"] == 0 for s in st)}
+            "fast_path": all(s["exact_fallback"] == 0 for s in st),
+            "fixed_length_path": all(s["fixed_length"] == 1 for s in st)}
 
 
 def evaluate_scope(H, hf, payload, bits: int, n_want: int, reps: int, check=None) -> dict:
@@ -330,6 +331,14 @@ def main():
                                     syn_e.data, syn_e.bits, out_e, syn_e.decoded_bytes,
                                     lambda o: synth.verify_tiled(o, syn_e), ks, 2))
         dec_e.close()
+        # the same stream through the general pipeline (heads, exit merges,
+        # walks, tables, scans, emission): config 5's merge-density stress
+        dec_g = H.Decoder(local, flags=H.FLAG_NO_FIXED)
+        dec_g.set_tree(syn_e.tree)
+        more.append(device_workload(f"synthetic {a.size_mib} MiB E.coli-tiled .huff, general pipeline "
+                                    f"(HH_FLAG_NO_FIXED)", dec_g, syn_e.data, syn_e.bits, out_e,
+                                    syn_e.decoded_bytes, lambda o: synth.verify_tiled(o, syn_e), ks, 2))
+        dec_g.close()
         del out_e, syn_e
         torch.cuda.empty_cache()
         iid = synth.iid_stream(hf, text, target, device=dev)

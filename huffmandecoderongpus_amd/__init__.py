@@ -77,6 +77,8 @@ class _RangeOut(C.Structure):
 
 
 FLAG_FORCE_EXACT = 1
+FLAG_FORCE_SEGMENT = 2
+FLAG_NO_FIXED = 4     # HH_FLAG_NO_FIXED: fixed-length codes through the general pipeline too
 _lib_handle: Optional[C.CDLL] = None
 
 # exported symbols and their ctypes signatures; tests check every one of these
