@@ -599,57 +599,6 @@ HH_HD hh_wk hh_walk_exits(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x, c
     return r;   /* k == 0: no merge within HH_KM regions */
 }
 
-/* k_walk's form: region j+1 with two pointers (W from x against region
- * j+1's own chain from its entry point y1 -- most walks meet it within a
- * few lookups), the regions after it by exit comparison (hh_walk_exits).
- * The same (k, e, cov, delta) as hh_walk. */
-HH_HD hh_wk hh_walk_mixed(const hh_ctx *c, uint32_t j, uint32_t S, uint32_t x, uint32_t y1,
-                          const uint32_t *xr, const uint32_t *nr) {
-    hh_wk r = {0u, 0u, 0u, 0, 0u, 0u};
-    const uint32_t bt = c->bt;
-    const uint32_t R = (j + 1) * S;
-    const uint32_t Ec = R + S < bt ? R + S : bt;
-    uint32_t A = x < bt ? x : bt, B = y1 < bt ? y1 : bt, ca = 0, cb = 0;
-    const uint32_t e = A > R ? A - R : 0u;
-    for (;;) {
-        if (A == B) {
-            r.k = 1;
-            r.e = e;
-            r.delta = (int32_t)ca - (int32_t)cb;
-            return r;
-        }
-        const bool mvA = A < B;
-        const uint32_t P = mvA ? A : B, Q = mvA ? B : A;
-        if (P >= Ec) break;                  /* both past the region end: covered */
-        const uint32_t tgt = Q < Ec ? Q : Ec;
-        hh_look L = hh_lookup(c, P);
-        const uint32_t o = hh_first_ge(L, tgt - P);
-        const uint32_t n = hh_syms_before(L, o);
-        uint32_t np = P + o;
-        if (np > bt) np = bt;
-        if (mvA) { A = np; ca += n; } else { B = np; cb += n; }
-    }
-    /* W left region j+1 at A (its first boundary at or past the region end)
-     * with ca symbols in it: the regions after it by their exits */
-    for (uint32_t k = 2; k <= HH_KM; k++) {
-        const uint32_t Rk = (j + k) * S;
-        const uint32_t Ek = Rk + S < bt ? Rk + S : bt;
-        const uint32_t ek = A > Rk ? A - Rk : 0u;
-        uint32_t n = 0;
-        if (A < Ek) A = hh_region_count(c, A, Ek, &n);
-        const uint32_t xk = xr[k] < bt ? xr[k] : bt;
-        if (A == xk) {
-            r.k = k;
-            r.e = ek;
-            r.cov = ca;
-            r.delta = (int32_t)n - (int32_t)nr[k];
-            return r;
-        }
-        ca += n;
-    }
-    return r;
-}
-
 /* ------------------------------------------------------------------ */
 /* Tile transfer table.  The state entering a tile is (d, e, delta):    */
 /* regions 0..d-1 are covered by the previous tile's last walk, the     */

@@ -180,12 +180,6 @@ int64_t hh_emu_decode_range(const int32_t *izero, const int32_t *ione, const uin
                 cw.sw = 1024;
                 cw.nls = 64;
                 const hh_wk we = hh_walk_exits(&cw, j, S, xs[j], xr, nr);
-                const hh_wk wm = hh_walk_mixed(&cw, j, S, xs[j], ynext, xr, nr);
-                if (wm.k != ref.k || (ref.k && (wm.e != ref.e || wm.cov != ref.cov || wm.delta != ref.delta))) {
-                    fprintf(stderr, "emu: tile %lu lane %u mixed walk (k %u e %u cov %u delta %d) vs mask walk (k %u e %u cov %u delta %d)\n",
-                            (unsigned long)t, j, wm.k, wm.e, wm.cov, wm.delta, ref.k, ref.e, ref.cov, ref.delta);
-                    return HH_ERR_INTERNAL - 503;
-                }
                 if (we.k != ref.k || (ref.k && (we.e != ref.e || we.cov != ref.cov || we.delta != ref.delta))) {
                     fprintf(stderr, "emu: tile %lu lane %u exit walk (k %u e %u cov %u delta %d) vs mask walk (k %u e %u cov %u delta %d)\n",
                             (unsigned long)t, j, we.k, we.e, we.cov, we.delta, ref.k, ref.e, ref.cov, ref.delta);
