@@ -35,6 +35,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <thread>
+
 #include "hh_algo.h"
 #include "hh_internal.h"
 #include "hiphuff.h"
@@ -1987,6 +1990,28 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
 // out of) pinned memory overlaps the DMA of the other, both ways.  Device
 // buffers are kept too: no allocation after the first call of a size.
 #define HH_HOST_CHUNK ((size_t)64 << 20)
+#define HH_HOST_THREADS 8                  // CPU copies into / out of pinned memory
+
+// The CPU side of a chunk: a single core copies ~10 GB/s, below PCIe's
+// rate, so the chunk is split over a few threads.
+static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t len) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t nt = std::min<size_t>(hw ? std::min<unsigned>(hw, HH_HOST_THREADS) : 1, len >> 20);
+    if (nt <= 1) {
+        memcpy(dst, src, len);
+        return;
+    }
+    std::thread th[HH_HOST_THREADS];
+    const size_t part = (len / nt + 4095) & ~(size_t)4095;
+    for (size_t i = 1; i < nt; i++) {
+        const size_t o = i * part;
+        if (o < len) th[i] = std::thread(memcpy, dst + o, src + o, std::min(part, len - o));
+    }
+    memcpy(dst, src, std::min(part, len));
+    for (size_t i = 1; i < nt; i++)
+        if (th[i].joinable()) th[i].join();
+}
+
 static int host_pipe(hh_decoder *d, uint8_t *host, uint8_t *dev, size_t n, bool h2d) {
     if (!n) return HH_OK;
     const size_t nch = (n + HH_HOST_CHUNK - 1) / HH_HOST_CHUNK;
@@ -1997,7 +2022,7 @@ static int host_pipe(hh_decoder *d, uint8_t *host, uint8_t *dev, size_t n, bool 
             uint8_t *pin = d->h_stage + (i & 1) * HH_HOST_CHUNK;
             if (i >= 2) HIP_OK(hipEventSynchronize(d->h_ev[i & 1]));   // buffer free again
             if (h2d) {
-                memcpy(pin, host + off, len);
+                par_memcpy(pin, host + off, len);
                 HIP_OK(hipMemcpyAsync(dev + off, pin, len, hipMemcpyHostToDevice, d->stream));
             } else {
                 HIP_OK(hipMemcpyAsync(pin, dev + off, len, hipMemcpyDeviceToHost, d->stream));
@@ -2009,7 +2034,7 @@ static int host_pipe(hh_decoder *d, uint8_t *host, uint8_t *dev, size_t n, bool 
             const size_t k = i - 1, off = k * HH_HOST_CHUNK;
             const size_t len = n - off < HH_HOST_CHUNK ? n - off : HH_HOST_CHUNK;
             HIP_OK(hipEventSynchronize(d->h_ev[k & 1]));
-            memcpy(host + off, d->h_stage + (k & 1) * HH_HOST_CHUNK, len);
+            par_memcpy(host + off, d->h_stage + (k & 1) * HH_HOST_CHUNK, len);
         }
     }
     return HH_OK;
