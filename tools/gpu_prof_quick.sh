@@ -1,5 +1,6 @@
 # Per-kernel device time of the decode pipeline (rocprofv3 kernel trace) on
-# the 1 GiB kjv-tiled stream, plus the diagnostic build's phase fractions.
+# the 1 GiB kjv-tiled stream, plus the diagnostic build's phase fractions
+# (build it first: make variant V=diag HIPEXTRA=-DHH_DIAG).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

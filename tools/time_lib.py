@@ -66,7 +66,7 @@ if os.environ.get("HH_DIAG"):            # a -DHH_DIAG build: phase cycles and w
     cyc = [buf[i] for i in range(6)]
     tot = sum(cyc) or 1
     res["front_phase_frac"] = {n: round(cyc[i] / tot, 3) for n, i in
-                               (("stage", 0), ("pass1", 1), ("walks", 2), ("table", 3))}
+                               (("stage", 0), ("pass1", 1), ("merge_defer", 2), ("records", 3))}
     ecyc = [buf[i] for i in (6, 7, 12, 13, 14)]
     etot = sum(ecyc) or 1
     res["emit_phase_frac"] = {n: round(v / etot, 3) for n, v in
