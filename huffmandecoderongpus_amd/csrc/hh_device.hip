@@ -49,8 +49,9 @@
 // ms; 16 with the 12-bit L1: 1.43 ms).
 #define HH_EMIT_NW_MAX 16
 #ifndef HH_FW
-#define HH_FW 4                     // waves per workgroup (k_front); 5 and 6 measured slower
-                                    // (a 5-wave workgroup puts two waves on one SIMD)
+#define HH_FW 8                     // waves per workgroup (k_front), sharing the 16 KiB F: 3
+                                    // workgroups per CU (with the 13-bit F, 4 / 7 / 8 / 14 waves:
+                                    // front + walks 1.29 / 1.21 / 1.13 / 1.26 ms)
 #endif
 #define HH_SCAN_TB 1024             // tiles per k_scan1 block
 #define HH_SCAN_BACK 4096           // longest non-CONST chain k_scan1 composes (else host scan)
@@ -280,8 +281,8 @@ __host__ __device__ constexpr uint32_t ftab_words(uint32_t fdir, uint32_t l2) {
 }
 
 #ifndef HH_FRONT_MINB
-#define HH_FRONT_MINB 4   // workgroups per CU the front kernel's registers are sized for (it
-                          // compiles to ~68 VGPRs: 7 waves per SIMD, as many as its LDS allows)
+#define HH_FRONT_MINB 2   // workgroups per CU the front kernel's registers are sized for (it
+                          // compiles to ~70 VGPRs: up to 7 waves per SIMD; its LDS allows 6)
 #endif
 
 // Diagnostic build only (-DHH_DIAG): every wave stamps the shader clock
