@@ -614,11 +614,14 @@ __global__ __launch_bounds__(64 * HH_TABLE_W) void k_table(Geometry geo, Work wk
     const uint64_t step = (uint64_t)gridDim.x * HH_TABLE_W;
     uint64_t t = (uint64_t)blockIdx.x * HH_TABLE_W + wv;
     const uint64_t tlast = geo.ntiles - 1;
+    // records loaded two tiles ahead
+    auto clampt = [&](uint64_t tt) { return tt < tlast ? tt : tlast; };
     uint32_t rec_n = t < geo.ntiles ? wk.recs[t * HH_NR + j] : 0u;
+    uint32_t rec_n2 = t < geo.ntiles ? wk.recs[clampt(t + step) * HH_NR + j] : 0u;
     for (; t < geo.ntiles; t += step) {
         const uint32_t rec = rec_n;
-        const uint64_t tn = t + step < tlast ? t + step : tlast;   // the next tile's record, ahead
-        rec_n = wk.recs[tn * HH_NR + j];
+        rec_n = rec_n2;
+        rec_n2 = wk.recs[clampt(t + 2 * step) * HH_NR + j];
         const uint32_t kk = rec_k(rec), e = rec_e(rec);
         const int32_t delta = rec_delta(rec);
         const int32_t charged = (int32_t)rec_nc(rec) + delta;
