@@ -1128,8 +1128,22 @@ __global__ __launch_bounds__(256) void k_fixed(const uint32_t *__restrict__ gdat
     __syncthreads();
     const uint64_t nfull = bits / L;                    // whole codes
     const uint32_t mask = (1u << L) - 1u;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g * 16 < nsym;
-         g += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t G = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (L == 2 && a16) {
+        // (E.coli) four groups per pass, their words loaded together: one
+        // word -> four byte lookups -> one 16-B store each
+        for (; (g + 3 * G) * 16 + 16 <= nfull; g += 4 * G) {
+            uint32_t w[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; u++) w[u] = gdata[g + u * G];
+#pragma unroll
+            for (uint32_t u = 0; u < 4; u++)
+                *(u32x4 *)(out + (g + u * G) * 16) = (u32x4){s_b4[w[u] & 255u], s_b4[(w[u] >> 8) & 255u],
+                                                             s_b4[(w[u] >> 16) & 255u], s_b4[w[u] >> 24]};
+        }
+    }
+    for (; g * 16 < nsym; g += G) {
         const uint64_t i0 = g * 16, p0 = i0 * L;
         if (L == 2 && i0 + 16 <= nfull && a16) {       // (E.coli) one word, four byte lookups
             const uint32_t w = gdata[g];
