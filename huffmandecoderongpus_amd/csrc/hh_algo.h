@@ -408,7 +408,13 @@ HH_HD uint32_t hh_region_head(const hh_ctx *c, uint32_t s, uint32_t R, uint64_t 
     return u.p < c->bt ? u.p : c->bt;
 }
 
-/* The left chain C_j and the right chain C_{j+1} share a boundary in the
+/* Round 1's boundary-mask merge test and mask walk (below) are no longer on
+ * the kernels' path (k_front merges on exit == entry, k_walk compares exits);
+ * the emulator keeps them as the reference those are checked against, lane
+ * by lane, and k_front's walks with HH_FRONT_WALK > 0 use hh_walk's
+ * two-pointer mode.
+ *
+ * The left chain C_j and the right chain C_{j+1} share a boundary in the
  * overlap window [R - G, R) (R = the start of region j+1) iff C_j's mask
  * bits there meet C_{j+1}'s head bits: then the chains are identical from
  * that boundary on, C_j's exit is C_{j+1}'s entry point y, and the walk
