@@ -30,16 +30,21 @@ emu: $(EMU)
 $(BUILD):
 	mkdir -p $(BUILD)
 
-$(BUILD)/hh_huff.o: $(CSRC)/hh_huff.c $(CSRC)/hh_internal.h include/hiphuff.h | $(BUILD)
+$(BUILD)/hh_huff.o: $(CSRC)/hh_huff.c $(CSRC)/hh_internal.h $(CSRC)/hh_fsm.h include/hiphuff.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
 $(BUILD)/hh_plugin.o: $(CSRC)/hh_plugin.c include/hiphuff.h include/hiphuff_plugin.h | $(BUILD)
 	$(CC) $(CFLAGS) -c $< -o $@
 
-$(BUILD)/hh_device.o: $(CSRC)/hh_device.hip $(CSRC)/hh_algo.h $(CSRC)/hh_internal.h include/hiphuff.h | $(BUILD)
+$(BUILD)/hh_device.o: $(CSRC)/hh_device.hip $(CSRC)/hh_algo.h $(CSRC)/hh_internal.h $(CSRC)/hh_fsm_dev.h \
+                      $(CSRC)/hh_fsm.h $(CSRC)/hh_fsm_algo.h include/hiphuff.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/hh_device.o $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
+$(BUILD)/hh_fsm.o: $(CSRC)/hh_fsm.hip $(CSRC)/hh_fsm_dev.h $(CSRC)/hh_fsm.h $(CSRC)/hh_fsm_algo.h \
+                   $(CSRC)/hh_internal.h include/hiphuff.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/hh_device.o $(BUILD)/hh_fsm.o $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 
 $(CLI): $(PKG)/host/hh_cli.c $(LIB) include/hiphuff.h include/hiphuff_plugin.h
@@ -49,8 +54,8 @@ $(CLI): $(PKG)/host/hh_cli.c $(LIB) include/hiphuff.h include/hiphuff_plugin.h
 oracle:
 	$(MAKE) -C oracle
 
-$(EMU): tests/emu/hh_emu.cpp $(CSRC)/hh_algo.h $(CSRC)/hh_internal.h $(BUILD)/hh_huff.o
-	$(CXX) -O2 -fPIC -shared $(INC) -Wno-comment -o $@ tests/emu/hh_emu.cpp $(BUILD)/hh_huff.o
+$(EMU): tests/emu/hh_emu.cpp tests/emu/hh_fsm_emu.cpp $(CSRC)/hh_algo.h $(CSRC)/hh_fsm_algo.h $(CSRC)/hh_fsm.h $(CSRC)/hh_internal.h $(BUILD)/hh_huff.o
+	$(CXX) -O2 -fPIC -shared $(INC) -Wno-comment -o $@ tests/emu/hh_emu.cpp tests/emu/hh_fsm_emu.cpp $(BUILD)/hh_huff.o
 
 clean:
 	rm -rf $(BUILD) $(LIB) $(EMU)
@@ -62,7 +67,8 @@ clean:
 # -> build/libhiphuff_<name>.so (tools/ab.sh)
 variant: $(BUILD)/hh_plugin.o
 	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/hh_device.hip -o $(BUILD)/hh_device_$(V).o
+	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/hh_fsm.hip -o $(BUILD)/hh_fsm_$(V).o
 	$(CC) $(CFLAGS) $(HIPEXTRA) -c $(CSRC)/hh_huff.c -o $(BUILD)/hh_huff_$(V).o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/libhiphuff_$(V).so $(BUILD)/hh_device_$(V).o \
-	    $(BUILD)/hh_huff_$(V).o $^
+	    $(BUILD)/hh_fsm_$(V).o $(BUILD)/hh_huff_$(V).o $^
 .PHONY: variant

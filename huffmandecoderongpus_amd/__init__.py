@@ -63,7 +63,8 @@ class _Config(C.Structure):
 class _Stats(C.Structure):
     _fields_ = [("ms_total", C.c_double), ("ms_sync", C.c_double), ("ms_scan", C.c_double),
                 ("ms_emit", C.c_double), ("out_len", C.c_uint64), ("lanes", C.c_uint64),
-                ("repairs", C.c_uint64), ("exact_fallback", C.c_int), ("fixed_length", C.c_int)]
+                ("repairs", C.c_uint64), ("exact_fallback", C.c_int), ("fixed_length", C.c_int),
+                ("state_machine", C.c_int)]
 
 
 class _Range(C.Structure):
@@ -79,6 +80,7 @@ class _RangeOut(C.Structure):
 FLAG_FORCE_EXACT = 1
 FLAG_FORCE_SEGMENT = 2
 FLAG_NO_FIXED = 4     # HH_FLAG_NO_FIXED: fixed-length codes through the general pipeline too
+FLAG_LEGACY = 8       # HH_FLAG_LEGACY: round 2's pipeline instead of the state-machine decode
 _lib_handle: Optional[C.CDLL] = None
 
 # exported symbols and their ctypes signatures; tests check every one of these
@@ -119,6 +121,7 @@ _SIGS = {
                            C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
     "hipHuffApproach": ([C.c_void_p, C.c_void_p, C.c_void_p], None),
     "hh_debug_counters": ([C.c_void_p, C.c_void_p], C.c_int),
+    "hh_debug_fsm": ([C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
 }
 
 

@@ -39,6 +39,8 @@
 #include <thread>
 
 #include "hh_algo.h"
+#include "hh_fsm_algo.h"
+#include "hh_fsm_dev.h"
 #include "hh_internal.h"
 #include "hiphuff.h"
 
@@ -1402,6 +1404,10 @@ struct hh_decoder {
     hipEvent_t h_ev[2];
     void *d_in, *d_out;
     size_t d_in_size, d_out_size;
+    // the state-machine decode (hh_fsm.hip): tables, device copies, workspace
+    hh_fsm_tables *ft;
+    FsmDev fsm;
+    FsmWs fsm_ws;
 };
 
 static int ensure_dev(void **p, size_t *have, size_t need) {
@@ -1429,7 +1435,8 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
     }
     if (hipSetDevice(d->device) != hipSuccess) { free(d); return HH_ERR_DEVICE; }
     d->ht = (hh_tables *)calloc(1, sizeof(hh_tables));
-    if (!d->ht) { free(d); return HH_ERR_NOMEM; }
+    d->ft = (hh_fsm_tables *)calloc(1, sizeof(hh_fsm_tables));
+    if (!d->ht || !d->ft) { free(d->ht); free(d->ft); free(d); return HH_ERR_NOMEM; }
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&d->d_l1, sizeof(uint64_t) * HH_L1_SIZE) != hipSuccess ||
         hipMalloc(&d->d_l2, sizeof(uint32_t) * HH_L2_MAX) != hipSuccess ||
@@ -1478,7 +1485,10 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
     for (int i = 0; i < 4; i++)
         if (d->ev[i]) hipEventDestroy(d->ev[i]);
     if (d->stream) hipStreamDestroy(d->stream);
+    fsm_free(&d->fsm);
+    if (d->fsm_ws.p) hipFree(d->fsm_ws.p);
     free(d->ht);
+    free(d->ft);
     free(d);
 }
 
@@ -1552,6 +1562,15 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     d->G = hh_pick_overlap(d->ht);
     if (getenv("HH_OVERLAP")) d->G = (uint32_t)atoi(getenv("HH_OVERLAP")) & ~31u;   // experiments
     if (d->G > HH_GMAX || d->G + 32 > d->S) d->G = 0;
+    // the state machine (trees of at most HH_FSM_MAXS internal nodes)
+    fsm_free(&d->fsm);
+    if (d->S && hh_fsm_build(d->ht, d->S, d->ft) == HH_OK) {
+        uint32_t Gf = hh_fsm_pick_head(d->ht);
+        if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) & ~7u;   // experiments
+        if (Gf > d->S) Gf = 0;
+        const int urc = fsm_upload(&d->fsm, d->ft, Gf);
+        if (urc != HH_OK && urc != HH_ERR_UNSUPPORTED) return urc;
+    }
     d->have_tree = 1;
     return HH_OK;
 }
@@ -1935,6 +1954,21 @@ static int fixed_path(hh_decoder *d, const void *d_data, uint64_t bits, uint8_t 
     return HH_OK;
 }
 
+// The state-machine path (hh_fsm.hip) decodes whenever its tables exist
+// (trees of at most HH_FSM_MAXS internal nodes) and no other path is forced.
+static bool fsm_path_ok(const hh_decoder *d) {
+    return d->fsm.ok && !(d->cfg.flags & (HH_FLAG_LEGACY | HH_FLAG_FORCE_EXACT | HH_FLAG_FORCE_SEGMENT));
+}
+static void fsm_stats(hh_decoder *d, uint64_t bits, uint64_t total, const float *ms) {
+    d->stats.ms_sync = ms[0];
+    d->stats.ms_scan = ms[1];
+    d->stats.ms_emit = ms[2];
+    d->stats.ms_total = ms[0] + ms[1] + ms[2];
+    d->stats.lanes = (bits + d->S - 1) / d->S;
+    d->stats.out_len = total;
+    d->stats.state_machine = 1;
+}
+
 extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits, void *d_out,
                                 uint64_t cap, uint64_t *out_len, void *hip_stream) {
     if (!d || !out_len || (!d_data && bits) || (!d_out && cap)) return HH_ERR_ARG;
@@ -1950,6 +1984,27 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     if (d->fixed_len && !(d->cfg.flags & (HH_FLAG_NO_FIXED | HH_FLAG_FORCE_EXACT | HH_FLAG_FORCE_SEGMENT)))
         return fixed_path(d, d_data, bits, (uint8_t *)d_out, cap, out_len, st);
     const bool seg_ok = d->ht->maxlen <= HH_MAXLEN_FAST && !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
+    if (fsm_path_ok(d)) {
+        uint64_t total = 0;
+        uint32_t leave = 0, en = 0;
+        float ms[3] = {0, 0, 0};
+        const int rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, d_data, bits, 0, 0, 0, d_out, cap, st,
+                                  &total, &leave, &en, ms);
+        fsm_stats(d, bits, total, ms);
+        if (rc == HH_ERR_UNSUPPORTED) {
+            // chains that did not meet within HH_FSM_KM regions: a code that
+            // does not resynchronise
+            d->stats.repairs = 1;
+            if (seg_ok) {
+                d->stats.exact_fallback = 2;
+                return segment_path(d, d_data, bits, (uint8_t *)d_out, cap, out_len, st);
+            }
+            d->stats.exact_fallback = 1;
+            return stage_pipeline(d, d_data, (int64_t)bits, (uint8_t *)d_out, cap, out_len, st);
+        }
+        *out_len = total;
+        return rc;
+    }
     if (!fast_path_ok(d) || (d->cfg.flags & HH_FLAG_FORCE_SEGMENT)) {
         if (seg_ok) {
             d->stats.exact_fallback = 2;
@@ -1991,6 +2046,21 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
     memset(ro, 0, sizeof(*ro));
     ro->leave_state = ro->entry_state = rg->in_state;
     if (rg->bits_avail == 0) return HH_OK;
+    if (fsm_path_ok(d)) {
+        // states are state-machine states (0: the root, the stream start)
+        if (rg->in_state >= d->fsm.ns) return HH_ERR_ARG;
+        float ms[3] = {0, 0, 0};
+        const int rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, d_data, rg->bits_avail, rg->ntiles,
+                                  rg->in_state, rg->prologue, d_out, cap, st, &ro->out_len, &ro->leave_state,
+                                  &ro->entry_state, ms);
+        fsm_stats(d, rg->bits_avail, ro->out_len, ms);
+        // the state leaving a segment does not depend on how it was entered
+        // once the chains have met inside it; the entry after a prologue is
+        // checked against the predecessor's leave state by the caller
+        ro->const_seen = 1;
+        ro->entry_exact = rg->prologue == 0;
+        return rc;
+    }
     // segments need the fast path (tile tables, entry states); a tree it
     // does not support is decoded whole, unsharded
     if (!fast_path_ok(d) || hh_state_d(rg->in_state) >= HH_KM) return HH_ERR_UNSUPPORTED;
@@ -2241,4 +2311,13 @@ extern "C" int hh_debug_counters(hh_decoder *d, uint64_t *out16) {
     if (hipMemcpy(out16, d->d_dbg, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         return HH_ERR_DEVICE;
     return HH_OK;
+}
+
+// Diagnostic: the state-machine count pass's arrays of the last decode of
+// `ntiles` tiles (records, corrections, tile sums, leaving states).
+extern "C" int hh_debug_fsm(hh_decoder *d, uint64_t ntiles, uint32_t *rec, uint32_t *fx, int32_t *tsum,
+                            uint32_t *xs) {
+    if (!d) return HH_ERR_ARG;
+    HIP_OK(hipSetDevice(d->device));
+    return fsm_debug_arrays(&d->fsm_ws, ntiles, rec, fx, tsum, xs);
 }

@@ -1,0 +1,73 @@
+/*
+ * hh_fsm.h -- the decode state machine (round 3's decode path).  Not part
+ * of the public ABI; shared by the host table builder (hh_huff.c), the HIP
+ * kernels (hh_fsm.hip) and the test emulator (tests/emu/hh_emu.cpp).
+ *
+ * The reference decodes bit by bit down the tree from every offset
+ * (decodeallbits.cl:10-33).  A chain's position inside the tree at a bit
+ * position p is a STATE: the internal node it has reached (0 = the root, i.e.
+ * p is a code boundary).  Stepping a state over the next k stream bits is a
+ * table lookup, independent of where codes start, so a decode step needs no
+ * data-dependent bit cursor: the step positions are fixed, only the state
+ * chains through the lookups.  Two chains that are in the same state at the
+ * same position are identical from there on, so "the speculative chain has
+ * met the true one" is a state comparison (the FSM form of makebigtable's
+ * pointer doubling, makebigtable.cl:10-40).
+ *
+ * States are numbered 0..ns-1 (internal nodes of the compact tree, BFS
+ * order, root first); ns <= HH_FSM_MAXS keeps a state in 8 bits.
+ *
+ *   ct[s * 256 + b]   u16: 8-bit steps (count pass): the state after the 8
+ *                     stream bits b (stream bit p in bit 0, the reference's
+ *                     LSB-first order, decodeallbits.cl:23) | the codes
+ *                     completed on the way << 8
+ *   b1[s * 2 + bit]   u32: 1-bit steps (the stream's last partial byte):
+ *                     next state | completed << 8 | the symbol << 16
+ *   tsym[s]           the sym byte of the state's node: the symbol the
+ *                     reference emits for a code cut off by the end of the
+ *                     stream (its tail rule, decodeallbits.cl:20-31)
+ *   et[s << K | v]    u64: K-bit steps (emission), v = the next K bits
+ *       bits  0..31   the symbols completed (first in bits 0..7, unused
+ *                     bytes 0): K = 6 for codes of >= 2 bits (<= 3
+ *                     symbols), K = 4 when a code has 1 bit (<= 4)
+ *       bits 32..55   the next state's row in et, in bytes: next << (K + 3)
+ *       bits 56..58   the number of symbols
+ *   er[s << r | v]    u64: the r-bit step that ends a region of S bits when K
+ *                     does not divide S (r = S mod K, 0: none); same layout,
+ *                     rows in et units
+ */
+#ifndef HH_FSM_H_
+#define HH_FSM_H_
+
+#include <stdint.h>
+
+#define HH_FSM_MAXS 255
+
+typedef struct {
+    uint32_t ns;              /* states (internal nodes)                      */
+    uint32_t K;               /* emission step bits                           */
+    uint32_t r;               /* remainder step bits of a region (S mod K)    */
+    uint32_t S;               /* region bits the remainder table is built for */
+    uint16_t ct[HH_FSM_MAXS * 256];
+    uint32_t b1[HH_FSM_MAXS * 2];
+    uint8_t tsym[HH_FSM_MAXS + 1];
+    uint64_t et[HH_FSM_MAXS * 64];
+    uint64_t er[HH_FSM_MAXS * 32];
+} hh_fsm_tables;
+
+#define HH_FSM_ET_SYMS(e) ((uint32_t)(e))
+#define HH_FSM_ET_ROW(e) ((uint32_t)((e) >> 32) & 0xffffffu)
+#define HH_FSM_ET_NSYM(e) ((uint32_t)((e) >> 56) & 7u)
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Builds the state machine of the compact tree in T (hh_tables_build) for
+ * regions of S bits.  HH_ERR_UNSUPPORTED when the tree has more than
+ * HH_FSM_MAXS internal nodes. */
+int hh_fsm_build(const void *T /* const hh_tables* */, uint32_t S, hh_fsm_tables *F);
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,806 @@
+// hh_fsm.hip -- the state-machine decode (gfx950), the decoder's main path.
+//
+// Three kernels on one stream (tables and per-lane rules: hh_fsm.h,
+// hh_fsm_algo.h):
+//
+//   k_cnt     one tile (64 regions of S bits) per WAVE, persistent grid:
+//             lane j holds region j's words and region j+1's in registers;
+//             (decodeallbits) the guess for region j+1 from a G-bit head,
+//             the region's count and exit state in 8-bit steps of the count
+//             table; (makebigtable) walks where an exit state differs from
+//             the next region's guess, repeated while a walk does not meet
+//             within its region; the next tile's corrections (lane 63);
+//             per region (entering state, count) -> HBM
+//   k_fscan1/2 the exclusive prefix of the tiles' counts (calcbitsindex /
+//             findmax)
+//   k_emf     one tile per wave again: each lane runs the state machine over
+//             its region from its true entering state in K-bit steps of the
+//             emission table, storing each step's symbols (up to 4 bytes) with
+//             one 4-byte LDS store at its output offset in the wave's staging
+//             buffer; the wave copies the tile's output out with 16-B stores
+//             (calcresult)
+//
+// No step needs a bit cursor: the step positions are compile-time, only the
+// state chains through the table lookups.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "hh_fsm_algo.h"
+#include "hh_fsm_dev.h"
+#include "hiphuff.h"
+
+#define FS_OK(x)                                                              \
+    do {                                                                      \
+        hipError_t e_ = (x);                                                  \
+        if (e_ != hipSuccess) {                                               \
+            fprintf(stderr, "hiphuff: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+            return HH_ERR_DEVICE;                                             \
+        }                                                                     \
+    } while (0)
+
+#define NR 64                 // regions per tile (a wave)
+#define CW 8                  // k_cnt: waves per workgroup
+#define EW 16                 // k_emf: waves per workgroup
+#define OBW 6144              // k_emf: output staging per wave (bytes); a kjv tile's output is ~3.7 KB
+#define SCAN_TB 1024          // tiles per k_fscan1 block
+#define FX_W 8                // corrections per tile (HH_FSM_KM)
+static_assert(FX_W == HH_FSM_KM, "corrections per tile");
+
+enum { FF_FAIL = 1, FF_OVER = 2 };
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32u __attribute__((aligned(1)));   // an LDS word at any byte address
+
+struct FsmGeo {
+    uint64_t bits;        // stream length of the segment
+    uint64_t nwords;      // readable payload words
+    uint64_t ntiles;
+    uint64_t emit_from;   // tiles before it are a prologue
+    uint32_t S, G, in_state, ns, r;
+};
+
+// Workspace (fsm_decode).  Nothing needs zeroing but `flags`.
+struct FsmWork {
+    uint32_t *flags;      // [0] status, [2..3] total, [4] leave state, [5] entry state
+    uint32_t *rec;        // [ntiles][NR] entering state | count << 8
+    int32_t *tsum;        // [ntiles] the tile's count (its own view of region 0)
+    uint32_t *xs;         // [ntiles] the state leaving the tile
+    uint32_t *fx;         // [ntiles + 1][FX_W] corrections of a tile's first regions
+    int32_t *lex;         // [ntiles + 1] exclusive prefix within the scan block
+    int64_t *blk;         // [nblk] block totals, then block bases
+};
+
+struct FsmTab {
+    const uint16_t *ct;
+    const uint32_t *b1;
+    const uint8_t *tsym;
+    const uint64_t *et;
+    const uint64_t *er;
+};
+
+// ---------------------------------------------------------------------------
+// wave helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t wave_incl_scan(int32_t x) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ int32_t wave_sum(int32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1, 64); }
+
+#define WAVE_SYNC()                                                    \
+    do {                                                               \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");         \
+        __builtin_amdgcn_wave_barrier();                               \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");         \
+    } while (0)
+
+// Words of a tile through a buffer resource over the readable words: loads
+// past the payload return 0 (never read as stream bits).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t fs_rsrc(const uint32_t *g, uint64_t w0, uint64_t nok) {
+    const uint64_t left = nok > w0 ? nok - w0 : 0u;
+    const uint32_t nbytes = left > 0x3fffffffull ? 0xfffffffcu : (uint32_t)left * 4u;
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(g + w0), 0, (int)nbytes, 0x00020000);
+}
+// SW words from word offset wo of the resource
+template <uint32_t SW>
+__device__ __forceinline__ void fs_load(uint32_t *v, __amdgpu_buffer_rsrc_t rs, uint32_t wo) {
+    if (SW % 4 == 0) {
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k += 4) {
+            const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, 0));
+            v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * (wo + k)), 0, 0);
+    }
+}
+
+// byte k / bits [q, q+n) of a region held in registers (compile-time k, q)
+template <uint32_t SW>
+__device__ __forceinline__ uint32_t rbyte(const uint32_t *w, uint32_t k) {
+    return __builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 8);
+}
+template <uint32_t SW>
+__device__ __forceinline__ uint32_t rbits(const uint32_t *w, uint32_t q, uint32_t n) {
+    const uint32_t i = q >> 5, o = q & 31;
+    if (o + n <= 32 || i + 1 >= SW) return __builtin_amdgcn_ubfe(w[i], o, n);
+    return __builtin_amdgcn_alignbit(w[i + 1], w[i], o) & ((1u << n) - 1u);
+}
+// bit q of a region held in registers, q not a compile-time constant (rare paths)
+template <uint32_t SW>
+__device__ __forceinline__ uint32_t rbit_dyn(const uint32_t *w, uint32_t q) {
+    uint32_t x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SW; k++) x = (q >> 5) == k ? w[k] : x;
+    return (x >> (q & 31)) & 1u;
+}
+
+// count table: next state | completed << 8, at LDS address 0
+__device__ __forceinline__ uint32_t ct_at(const uint8_t *lds, uint32_t s, uint32_t b) {
+    return *(const uint16_t *)(lds + ((s << 9) | (b << 1)));
+}
+
+// ---------------------------------------------------------------------------
+// Region passes of k_cnt on words in registers.  lim: the region's readable
+// bits (S unless the stream ends inside it); TAIL instantiations check it.
+// ---------------------------------------------------------------------------
+// Count of a region entered in state s; returns the exit state.
+template <uint32_t SW, bool TAIL>
+__device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
+                                               uint32_t s, uint32_t lim, uint32_t *n) {
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4 * SW; k++) {
+        if (!TAIL || 8 * k + 8 <= lim) {
+            const uint32_t e = ct_at(lds, s, rbyte<SW>(w, k));
+            s = e & 255u;
+            c += e >> 8;
+        }
+    }
+    if (TAIL) {
+        for (uint32_t q = lim & ~7u; q < lim; q++) {       // the last partial byte, bit by bit
+            const uint32_t e = b1[s * 2 + rbit_dyn<SW>(w, q)];
+            s = e & 255u;
+            c += (e >> 8) & 255u;
+        }
+    }
+    *n = c;
+    return s;
+}
+
+// Walk: chains A and B stepped together over a region until they meet
+// (their count difference stops changing then); lanes not walking carry
+// A == B.  Returns 1 if every lane met; the caller checks A == B per lane.
+template <uint32_t SW, bool TAIL>
+__device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
+                                            uint32_t &A, uint32_t &B, int32_t &d, uint32_t lim) {
+    bool go = true;                                   // (uniform) some lane has not met yet
+#pragma unroll
+    for (uint32_t k = 0; k < 4 * SW; k++) {
+        if (go && (!TAIL || 8 * k + 8 <= lim)) {
+            const uint32_t x = rbyte<SW>(w, k);
+            const uint32_t ea = ct_at(lds, A, x), eb = ct_at(lds, B, x);
+            A = ea & 255u;
+            B = eb & 255u;
+            d += (int32_t)(ea >> 8) - (int32_t)(eb >> 8);
+        }
+        if ((k & 3) == 3 && go) go = __ballot(A != B) != 0;
+    }
+    if (TAIL) {
+        for (uint32_t q = lim & ~7u; q < lim && A != B; q++) {
+            const uint32_t x = rbit_dyn<SW>(w, q);
+            const uint32_t ea = b1[A * 2 + x], eb = b1[B * 2 + x];
+            A = ea & 255u;
+            B = eb & 255u;
+            d += (int32_t)((ea >> 8) & 255u) - (int32_t)((eb >> 8) & 255u);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_cnt: the count pass of every tile, one tile per wave.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns) {
+    return ((ns * 512u + ns * 8u + ns) + 15u) & ~15u;
+}
+
+
+// One tile of the count pass (TAIL: the stream ends in this tile or in the
+// next tile's first region).  w: region j's words, nx: region j+1's (lane 63:
+// the next tile's region 0).
+template <uint32_t SW, bool TAIL>
+__device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
+                                         const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
+                                         const uint32_t *nx) {
+    constexpr uint32_t S = 32 * SW;
+    const uint32_t j = threadIdx.x & 63u;
+    const uint64_t TB = (uint64_t)NR * S, T0 = t * TB;
+    const uint64_t R = T0 + (uint64_t)j * S;
+    // readable bits of region j and of region j+1
+    uint32_t lim = S, limn = S;
+    if (TAIL) {
+        lim = R >= geo.bits ? 0u : (geo.bits - R < S ? (uint32_t)(geo.bits - R) : S);
+        limn = R + S >= geo.bits ? 0u : (geo.bits - R - S < S ? (uint32_t)(geo.bits - R - S) : S);
+    }
+    const bool has_next = t + 1 < geo.ntiles;
+
+    // decodeallbits: the guess for region j+1 (a chain started at the root G
+    // bits before it), then region j from the guess lane j-1 made for it
+    uint32_t gs = 0;
+    if (geo.G) {
+        const uint32_t GB = geo.G >> 3;
+#pragma unroll
+        for (uint32_t k = 4 * SW - 8; k < 4 * SW; k++) {
+            gs = k == 4 * SW - GB ? 0u : gs;
+            gs = ct_at(lds, gs, rbyte<SW>(w, k)) & 255u;
+        }
+    }
+    const uint32_t sp = j ? shfl_up1(gs) : (t == 0 ? geo.in_state : 0u);
+    uint32_t n;
+    uint32_t X = cnt_region<SW, TAIL>(lds, F.b1, w, sp, lim, &n);   // region j's exit (given its entry)
+
+    // makebigtable: where region j's exit differs from the entry assumed for
+    // region j+1 (E), lane j walks region j+1 with both chains; their count
+    // difference up to where they meet corrects region j+1's count, and E
+    // becomes the exit.  A walk that does not meet in its region changes that
+    // region's exit: the next lane walks again in the next round.  The
+    // corrections telescope: d = count(true chain) - count(first assumption).
+    uint32_t E = j == 63 ? 0u : gs;
+    int32_t d = 0;
+    bool lost = false;                              // lane 63: not met in the next tile's region 0
+    for (int round = 0; round < NR; round++) {
+        const bool want = X != E && limn > 0 && (j < 63 || has_next);
+        if (__ballot(want) == 0) break;
+        uint32_t A = X, B = want ? E : X;           // (not walking: A == B, no change)
+        int32_t dd = 0;
+        walk_region<SW, TAIL>(lds, F.b1, nx, A, B, dd, limn);
+        bool deep = false;
+        if (want) {
+            if (TAIL && A != B && limn < S) dd += (int32_t)(A != 0) - (int32_t)(B != 0);   // tail rule
+            d += dd;
+            E = X;
+            deep = A != B && limn == S;
+            if (j == 63 && deep) {
+                lost = true;
+                deep = false;
+            }
+        }
+        const uint32_t dp = shfl_up1(deep ? 1u : 0u), xa = shfl_up1(A);
+        if (j > 0 && dp) X = xa;
+    }
+
+    // records: region j entered in the state lane j-1 assumed last
+    const uint32_t ent = j ? shfl_up1(E) : sp;
+    const uint32_t cnt = (uint32_t)((int32_t)n + (j ? (int32_t)shfl_up1((uint32_t)d) : 0));
+    wk.rec[t * NR + j] = fsm_rec(ent, cnt);
+    const int32_t sum = wave_sum((int32_t)cnt);
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
+    if (j == 0) {
+        wk.tsum[t] = sum;
+        wk.xs[t] = x;
+    }
+    // the next tile's corrections (its region 0 assumed entered at the root)
+    if (t == 0 && j < FX_W) wk.fx[j] = 0u;
+    if (has_next) {
+        const bool lst = __builtin_amdgcn_readlane((int)lost, 63) != 0;
+        if (!lst) {
+            const uint32_t E63 = (uint32_t)__builtin_amdgcn_readlane((int)E, 63);
+            const int32_t d63 = __builtin_amdgcn_readlane(d, 63);
+            if (j < FX_W) wk.fx[(t + 1) * FX_W + j] = j == 0 && (E63 | (uint32_t)d63) ? fsm_fx(E63, d63) : 0u;
+        } else if (j == 0) {
+            // rare: the chains meet beyond the next tile's region 0 (words
+            // from global memory)
+            uint32_t f[FX_W];
+            if (!fsm_fix_next(&F, g, T0 + TB, S, geo.bits, x, f)) atomicOr(wk.flags, (uint32_t)FF_FAIL);
+            for (int i = 0; i < FX_W; i++) wk.fx[(t + 1) * FX_W + i] = f[i];
+        }
+    }
+}
+
+template <uint32_t SW>
+__global__ __launch_bounds__(64 * CW) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr uint32_t S = 32 * SW;
+    const uint32_t ns = geo.ns, tid = threadIdx.x, j = tid & 63u, wv = tid >> 6;
+    uint32_t *s_b1 = (uint32_t *)(smem + ns * 512);
+    uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
+    for (uint32_t i = tid; i < ns * 128; i += blockDim.x) ((uint32_t *)smem)[i] = ((const uint32_t *)tab.ct)[i];
+    for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
+    for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
+    __syncthreads();
+    const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts};
+    const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * CW;
+    // tiles whose regions (and the next tile's region 0) end before the stream
+    const uint64_t nfast = geo.bits >= TB + S ? (geo.bits - S) / TB : 0;
+    uint64_t t = (uint64_t)blockIdx.x * CW + wv;
+    // the next tile's words are loaded one tile ahead
+    uint32_t pw[SW], pn[SW];
+    auto prefetch = [&](uint64_t tt) {
+        const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
+        fs_load<SW>(pw, rs, j * SW);
+        fs_load<SW>(pn, rs, (j + 1) * SW);
+    };
+    if (t < geo.ntiles) prefetch(t);
+    for (; t < geo.ntiles; t += nwv) {
+        uint32_t w[SW], nx[SW];
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) {
+            w[k] = pw[k];
+            nx[k] = pn[k];
+        }
+        const uint64_t tn = t + nwv < geo.ntiles ? t + nwv : t;
+        prefetch(tn);
+        if (t < nfast) cnt_tile<SW, false>(smem, F, g, geo, wk, t, w, nx);
+        else cnt_tile<SW, true>(smem, F, g, geo, wk, t, w, nx);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fscan1 / k_fscan2: output base of every tile
+// ---------------------------------------------------------------------------
+// One thread per tile t in [0, ntiles]: the tile's count (its own view plus
+// the corrections its predecessor wrote; prologue tiles emit nothing), the
+// exclusive prefix within the block -> lex, the block total -> blk.
+__global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk) {
+    __shared__ int32_t s_tmp[SCAN_TB / 64];
+    const uint64_t t = (uint64_t)blockIdx.x * SCAN_TB + threadIdx.x;
+    int32_t c = 0;
+    if (t < geo.ntiles && t >= geo.emit_from) {
+        c = wk.tsum[t];
+#pragma unroll
+        for (int i = 0; i < FX_W; i++) c += fsm_fx_d(wk.fx[t * FX_W + i]);
+    }
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const int32_t x = wave_incl_scan(c);
+    if (lane == 63) s_tmp[wv] = x;
+    __syncthreads();
+    int32_t base = 0, tot = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < SCAN_TB / 64; i++) {
+        const int32_t v = s_tmp[i];
+        base += i < wv ? v : 0;
+        tot += v;
+    }
+    if (t <= geo.ntiles) wk.lex[t] = base + x - c;
+    if (threadIdx.x == 0) wk.blk[blockIdx.x] = tot;
+}
+
+// One block: block totals -> exclusive block bases; totals and states.
+__global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_t nblk) {
+    __shared__ int64_t s_w[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+    int64_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
+        const int64_t v = b0 + tid < nblk ? wk.blk[b0 + tid] : 0;
+        int64_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) s_w[wv] = x;
+        __syncthreads();
+        int64_t base = 0, tot = 0;
+        for (uint32_t i = 0; i < 16; i++) {
+            base += i < wv ? s_w[i] : 0;
+            tot += s_w[i];
+        }
+        if (b0 + tid < nblk) wk.blk[b0 + tid] = carry + base + x - v;
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        wk.flags[2] = (uint32_t)carry;
+        wk.flags[3] = (uint32_t)((uint64_t)carry >> 32);
+        wk.flags[4] = geo.ntiles ? wk.xs[geo.ntiles - 1] : geo.in_state;
+        uint32_t en = geo.in_state;
+        if (geo.emit_from < geo.ntiles) {
+            const uint32_t f = wk.fx[geo.emit_from * FX_W];
+            en = fsm_fx_ok(f) ? fsm_fx_ent(f) : fsm_rec_ent(wk.rec[geo.emit_from * NR]);
+        }
+        wk.flags[5] = en;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_emf: emission of every emitted tile, one tile per wave.
+// ---------------------------------------------------------------------------
+__host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, uint32_t r) {
+    return ((ns << K) * 8u + (r ? (ns << r) * 8u : 0u) + ns * 8u + ns + 15u) & ~15u;
+}
+
+// Region j entered in state s, its symbols to the staging from LDS byte
+// address oa on: K-bit steps, each step's symbols shifted into a 64-bit
+// accumulator whose low dword is stored to its aligned LDS dword every step
+// (a dword is stored again until it is full: no branch), then the r-bit
+// step; TAIL: steps while whole, the rest bit by bit, and the tail rule.
+// The unused bytes of every stored dword are zero: a dword shared with the
+// neighbouring runs is repaired by OR afterwards (emf_edges).  e4 receives
+// the first four steps' entries; *last the run's last dword value.
+template <uint32_t SW, uint32_t K, bool TAIL>
+__device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, uint32_t r, const uint32_t *b1,
+                                           const uint8_t *ts, const uint32_t *w, uint32_t s, uint32_t lim,
+                                           bool at_end, uint32_t oa, uint64_t *e4, uint32_t *lastw,
+                                           uint32_t *lastwd) {
+    constexpr uint32_t S = 32 * SW;
+    uint32_t row = s << (K + 3);
+    uint32_t wd = oa & ~3u, sh = (oa & 3u) * 8u;
+    uint64_t acc = 0;
+    auto put = [&](uint64_t e) {
+        acc |= (uint64_t)(uint32_t)e << sh;
+        *(uint32_t *)(lds + wd) = (uint32_t)acc;
+        sh += (uint32_t)(e >> 53) & 0x38u;          // 8 * nsym
+        const bool full = sh >= 32;
+        wd += full ? 4u : 0u;
+        acc = full ? acc >> 32 : acc;
+        sh &= 31u;
+    };
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) e4[i] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < S / K; k++) {
+        const uint32_t q = k * K;
+        if (!TAIL || q + K <= lim) {
+            const uint64_t e = *(const uint64_t *)(lds + row + (rbits<SW>(w, q, K) << 3));
+            put(e);
+            row = (uint32_t)(e >> 32) & 0xffffffu;
+            if (k < 4) e4[k] = e;
+        }
+    }
+    if (!TAIL) {
+        if (r) {
+            const uint64_t e = *(const uint64_t *)(lds + er_off + (row >> (K - r)) + (rbits<SW>(w, S - r, r) << 3));
+            put(e);
+            row = (uint32_t)(e >> 32) & 0xffffffu;
+        }
+    } else {
+        uint32_t st = row >> (K + 3);
+        for (uint32_t q = lim / K * K; q < lim; q++) {
+            const uint32_t v = b1[st * 2 + rbit_dyn<SW>(w, q)];
+            st = v & 255u;
+            put((uint64_t)((v >> 16) & 255u) | ((uint64_t)((v >> 8) & 255u) << 56));
+        }
+        row = st << (K + 3);
+    }
+    if (at_end && (row >> (K + 3)) != 0) put((uint64_t)ts[row >> (K + 3)] | (1ull << 56));   // the tail rule
+    *(uint32_t *)(lds + wd) = (uint32_t)acc;        // the bytes of the last step's overflow
+    *lastw = (uint32_t)acc;
+    *lastwd = wd;
+}
+
+// After every lane's stores: the dwords a run shares with its neighbours hold
+// one run's bytes (and zeros); each run ORs its own bytes back into its first
+// and last dword.  The first dword's bytes come from the first four steps'
+// entries (or, when those hold too few symbols, a bit-serial re-run).
+template <uint32_t SW, uint32_t K>
+__device__ __forceinline__ void emf_edges(uint8_t *lds, const uint32_t *b1, const uint8_t *ts, const uint32_t *w,
+                                          uint32_t s, uint32_t lim, bool at_end, uint32_t cnt, uint32_t oa,
+                                          const uint64_t *e4, uint32_t lastw, uint32_t lastwd) {
+    if (!cnt) return;
+    const uint32_t b0 = oa & 3u;
+    const uint32_t need = 4u - b0 < cnt ? 4u - b0 : cnt;   // the run's bytes in its first dword
+    uint64_t acc = 0;
+    uint32_t got = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+        if (got < 4) acc |= (uint64_t)(uint32_t)e4[i] << (8 * got);
+        got += (uint32_t)(e4[i] >> 56) & 7u;
+    }
+    if (got < need) {
+        acc = 0;
+        got = 0;
+        uint32_t st = s;
+        for (uint32_t q = 0; q < lim && got < need; q++) {
+            const uint32_t v = b1[st * 2 + rbit_dyn<SW>(w, q)];
+            st = v & 255u;
+            if ((v >> 8) & 255u) acc |= (uint64_t)((v >> 16) & 255u) << (8 * got++);
+        }
+        if (got < need && at_end && st != 0) acc |= (uint64_t)ts[st] << (8 * got++);
+    }
+    const uint32_t firstw = ((uint32_t)acc & (need == 4 ? 0xffffffffu : ((1u << (8 * need)) - 1u))) << (8 * b0);
+    atomicOr((uint32_t *)(lds + (oa & ~3u)), firstw);
+    if (lastwd != (oa & ~3u) && lastw) atomicOr((uint32_t *)(lds + lastwd), lastw);
+}
+
+// A region whose tile's output does not fit the staging buffer: its symbols
+// straight to HBM, bit by bit (rare).
+template <uint32_t SW>
+__device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts, const uint32_t *w, uint32_t s,
+                                           uint32_t lim, bool at_end, uint8_t *dst) {
+    uint32_t o = 0;
+    for (uint32_t q = 0; q < lim; q++) {
+        const uint32_t v = b1[s * 2 + rbit_dyn<SW>(w, q)];
+        s = v & 255u;
+        if ((v >> 8) & 255u) dst[o++] = (uint8_t)(v >> 16);
+    }
+    if (at_end && s != 0) dst[o] = ts[s];
+}
+
+template <uint32_t SW, uint32_t K>
+__global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+                                                 uint8_t *__restrict__ out, uint64_t cap) {
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr uint32_t S = 32 * SW;
+    const uint32_t ns = geo.ns, r = geo.r, tid = threadIdx.x, j = tid & 63u, wv = tid >> 6;
+    const uint32_t er_off = (ns << K) * 8u;
+    uint32_t *s_b1 = (uint32_t *)(smem + er_off + (r ? (ns << r) * 8u : 0u));
+    uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
+    const uint32_t stage = emf_tab_bytes(ns, K, r) + wv * OBW;           // the wave's staging (LDS byte address)
+    for (uint32_t i = tid; i < (ns << K); i += blockDim.x) ((uint64_t *)smem)[i] = tab.et[i];
+    for (uint32_t i = tid; r && i < (ns << r); i += blockDim.x) ((uint64_t *)(smem + er_off))[i] = tab.er[i];
+    for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
+    for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
+    __syncthreads();
+
+    const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * EW;
+    const uint64_t nfast = geo.bits / TB;         // tiles that end before the stream does
+    const uint64_t tlast = geo.ntiles - 1;        // (launched only when emit_from < ntiles)
+    // next tile's words, record, correction and base, loaded one tile ahead
+    // (the base words by lanes 0..2, read out with readlane where consumed)
+    uint32_t pw[SW], prec = 0, pfx = 0, pmeta = 0;
+    auto prefetch = [&](uint64_t tt) {
+        const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
+        prec = wk.rec[tt * NR + j];
+        pfx = wk.fx[tt * FX_W + (j & (FX_W - 1))];
+        const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / SCAN_TB);
+        const uint32_t ln = j & 3u;
+        pmeta = *(ln == 0 ? blk32 : ln == 1 ? blk32 + 1 : (const uint32_t *)&wk.lex[tt]);
+        fs_load<SW>(pw, rs, j * SW);
+    };
+    uint64_t t = geo.emit_from + (uint64_t)blockIdx.x * EW + wv;
+    if (t < geo.ntiles) prefetch(t);
+    for (; t < geo.ntiles; t += nwv) {
+        uint32_t w[SW];
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
+        const uint32_t rc = prec, fx = j < FX_W ? pfx : 0u;
+        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)pmeta, 0);
+        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)pmeta, 1);
+        const int32_t lx = __builtin_amdgcn_readlane((int)pmeta, 2);
+        prefetch(t + nwv < geo.ntiles ? t + nwv : tlast);
+        uint32_t ent = fsm_rec_ent(rc);
+        int32_t cnt = (int32_t)fsm_rec_cnt(rc);
+        if (fsm_fx_ok(fx)) {
+            ent = fsm_fx_ent(fx);
+            cnt += fsm_fx_d(fx);
+        }
+        const uint32_t c = (uint32_t)cnt;
+        const int32_t incl = wave_incl_scan((int32_t)c);
+        const uint32_t L = (uint32_t)incl - c;
+        const uint32_t Tout = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+        const uint64_t P0 = (uint64_t)((int64_t)(((uint64_t)bhi << 32) | blo) + lx);
+        const bool inside = P0 <= cap && Tout <= cap - P0;
+        if (j == 0 && !inside) atomicOr(wk.flags, (uint32_t)FF_OVER);
+        if (!inside) continue;
+        const uint64_t R = t * TB + (uint64_t)j * S;
+        uint32_t lim = S;
+        bool at_end = R + S == geo.bits;
+        const bool tail = t >= nfast;
+        if (tail) {
+            lim = R >= geo.bits ? 0u : (geo.bits - R < S ? (uint32_t)(geo.bits - R) : S);
+            at_end = R < geo.bits && R + S >= geo.bits;
+        }
+        const uint32_t a0 = (uint32_t)(P0 & 15u);
+        if (a0 + Tout + 8 <= OBW) {
+            const uint32_t oa = stage + a0 + L;
+            uint64_t e4[4];
+            uint32_t lw = 0, lwd = 0;
+            WAVE_SYNC();                              // the previous tile's copy-out has read the staging
+            if (!tail) emf_region<SW, K, false>(smem, er_off, r, s_b1, s_ts, w, ent, lim, at_end, oa, e4, &lw, &lwd);
+            else emf_region<SW, K, true>(smem, er_off, r, s_b1, s_ts, w, ent, lim, at_end, oa, e4, &lw, &lwd);
+            WAVE_SYNC();
+            emf_edges<SW, K>(smem, s_b1, s_ts, w, ent, lim, at_end, c, oa, e4, lw, lwd);
+            WAVE_SYNC();
+            // copy-out: whole 16-B blocks, the two partial ones byte by byte
+            uint8_t *gb = out + (P0 - a0);
+            const uint8_t *sb = smem + stage;
+            const uint32_t nq = (a0 + Tout + 15u) / 16u;
+            for (uint32_t i = j; i < nq; i += 64) {
+                const uint32_t lo = 16 * i;
+                if (lo >= a0 && lo + 16 <= a0 + Tout) {
+                    __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
+                } else {
+                    const uint32_t e = lo + 16 < a0 + Tout ? lo + 16 : a0 + Tout;
+                    for (uint32_t q = lo > a0 ? lo : a0; q < e; q++) gb[q] = sb[q];
+                }
+            }
+        } else {
+            emf_direct<SW>(s_b1, s_ts, w, ent, lim, at_end, out + P0 + L);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork);
+typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t);
+
+#define FSM_SW_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+static kcnt_t kcnt_for(uint32_t sw) {
+    switch (sw) {
+#define X(n) case n: return k_cnt<n>;
+        FSM_SW_CASES(X)
+#undef X
+    default: return nullptr;
+    }
+}
+static kemf_t kemf_for(uint32_t sw, uint32_t K) {
+    switch (sw) {
+#define X(n) case n: return K == 6 ? k_emf<n, 6> : K == 4 ? k_emf<n, 4> : nullptr;
+        FSM_SW_CASES(X)
+#undef X
+    default: return nullptr;
+    }
+}
+
+static size_t lds_cnt(const FsmDev *fd) { return cnt_tab_bytes(fd->ns); }
+static size_t lds_emf(const FsmDev *fd) { return emf_tab_bytes(fd->ns, fd->K, fd->r) + (size_t)EW * OBW; }
+
+void fsm_free(FsmDev *fd) {
+    if (fd->ct) (void)hipFree(fd->ct);
+    if (fd->b1) (void)hipFree(fd->b1);
+    if (fd->tsym) (void)hipFree(fd->tsym);
+    if (fd->et) (void)hipFree(fd->et);
+    if (fd->er) (void)hipFree(fd->er);
+    memset(fd, 0, sizeof(*fd));
+}
+
+int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G) {
+    fsm_free(fd);
+    const uint32_t ns = F->ns;
+    const uint32_t sw = F->S / 32;
+    if (F->S % 32 || sw < 2 || sw > 12 || G % 8 || G > 64 || G > F->S) return HH_ERR_UNSUPPORTED;
+    fd->ns = ns;
+    fd->K = F->K;
+    fd->r = F->r;
+    fd->S = F->S;
+    fd->G = G;
+    if (lds_emf(fd) > 160 * 1024 || lds_cnt(fd) > 160 * 1024) return HH_ERR_UNSUPPORTED;
+    FS_OK(hipMalloc(&fd->ct, (size_t)ns * 512));
+    FS_OK(hipMalloc(&fd->b1, (size_t)ns * 8));
+    FS_OK(hipMalloc(&fd->tsym, (size_t)ns + 1));
+    FS_OK(hipMalloc(&fd->et, (size_t)(ns << F->K) * 8));
+    FS_OK(hipMalloc(&fd->er, (size_t)(ns << (F->r ? F->r : 1)) * 8));
+    FS_OK(hipMemcpy(fd->ct, F->ct, (size_t)ns * 512, hipMemcpyHostToDevice));
+    FS_OK(hipMemcpy(fd->b1, F->b1, (size_t)ns * 8, hipMemcpyHostToDevice));
+    FS_OK(hipMemcpy(fd->tsym, F->tsym, (size_t)ns, hipMemcpyHostToDevice));
+    FS_OK(hipMemcpy(fd->et, F->et, (size_t)(ns << F->K) * 8, hipMemcpyHostToDevice));
+    if (F->r) FS_OK(hipMemcpy(fd->er, F->er, (size_t)(ns << F->r) * 8, hipMemcpyHostToDevice));
+    fd->ok = 1;
+    return HH_OK;
+}
+
+static int fsm_grids(FsmDev *fd) {
+    if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns) return HH_OK;
+    const uint32_t sw = fd->S / 32;
+    const kcnt_t kc = kcnt_for(sw);
+    const kemf_t ke = kemf_for(sw, fd->K);
+    if (!kc || !ke) return HH_ERR_UNSUPPORTED;
+    int pc = 0, pe = 0, ncu = 0, dev = 0;
+    FS_OK(hipGetDevice(&dev));
+    FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kc, 64 * CW, lds_cnt(fd)));
+    FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, ke, 64 * EW, lds_emf(fd)));
+    FS_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    if (pc < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
+    fd->grid_c = (uint32_t)(pc * ncu);
+    fd->grid_e = (uint32_t)(pe * ncu);
+    fd->sized_S = fd->S;
+    fd->sized_ns = fd->ns;
+    return HH_OK;
+}
+
+static int ws_need(FsmWs *ws, size_t need) {
+    if (ws->size >= need) return HH_OK;
+    if (ws->p) FS_OK(hipFree(ws->p));
+    ws->p = nullptr;
+    ws->size = 0;
+    const size_t sz = need + need / 8;
+    if (hipMalloc(&ws->p, sz) != hipSuccess) return HH_ERR_NOMEM;
+    ws->size = sz;
+    return HH_OK;
+}
+
+int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
+               uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
+               hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms) {
+    if (!fd->ok) return HH_ERR_UNSUPPORTED;
+    int rc = fsm_grids(fd);
+    if (rc) return rc;
+    if (in_state >= fd->ns) return HH_ERR_ARG;
+    FsmGeo geo;
+    geo.bits = bits;
+    geo.nwords = ((bits + 7) / 8 + HH_PAYLOAD_PAD) / 4;
+    geo.S = fd->S;
+    geo.G = fd->G;
+    geo.in_state = in_state;
+    geo.ns = fd->ns;
+    geo.r = fd->r;
+    const uint64_t TB = (uint64_t)NR * fd->S;
+    const uint64_t all = (bits + TB - 1) / TB;
+    geo.ntiles = ntiles && ntiles < all ? ntiles : all;
+    geo.emit_from = emit_from;
+    const uint64_t nt = geo.ntiles;
+    const uint32_t nblk = (uint32_t)((nt + 1 + SCAN_TB - 1) / SCAN_TB);
+    // workspace: flags 64 B | rec | tsum | xs | fx | lex | blk
+    const size_t o_rec = 64, o_tsum = o_rec + nt * NR * 4, o_xs = o_tsum + nt * 4, o_fx = o_xs + nt * 4;
+    const size_t o_lex = o_fx + (nt + 1) * FX_W * 4, o_blk = (o_lex + (nt + 1) * 4 + 7) & ~(size_t)7;
+    rc = ws_need(ws, o_blk + (size_t)nblk * 8);
+    if (rc) return rc;
+    uint8_t *w = (uint8_t *)ws->p;
+    FsmWork wk;
+    wk.flags = (uint32_t *)w;
+    wk.rec = (uint32_t *)(w + o_rec);
+    wk.tsum = (int32_t *)(w + o_tsum);
+    wk.xs = (uint32_t *)(w + o_xs);
+    wk.fx = (uint32_t *)(w + o_fx);
+    wk.lex = (int32_t *)(w + o_lex);
+    wk.blk = (int64_t *)(w + o_blk);
+    FsmTab tab = {fd->ct, fd->b1, fd->tsym, fd->et, fd->er};
+    const uint32_t sw = fd->S / 32;
+    const kcnt_t kc = kcnt_for(sw);
+    const kemf_t ke = kemf_for(sw, fd->K);
+    FS_OK(hipMemsetAsync(wk.flags, 0, 64, st));
+    FS_OK(hipEventRecord(ev[0], st));
+    {
+        const uint64_t nwg = (nt + CW - 1) / CW;
+        const uint32_t gc = (uint32_t)(nwg < fd->grid_c ? nwg : fd->grid_c);
+        hipLaunchKernelGGL(kc, dim3(gc), dim3(64 * CW), lds_cnt(fd), st, (const uint32_t *)d_data, geo, tab, wk);
+        FS_OK(hipGetLastError());
+    }
+    FS_OK(hipEventRecord(ev[1], st));
+    hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk);
+    FS_OK(hipGetLastError());
+    hipLaunchKernelGGL(k_fscan2, dim3(1), dim3(1024), 0, st, geo, wk, nblk);
+    FS_OK(hipGetLastError());
+    FS_OK(hipEventRecord(ev[2], st));
+    if (emit_from < nt) {
+        const uint64_t ne = nt - emit_from, nwg = (ne + EW - 1) / EW;
+        const uint32_t ge = (uint32_t)(nwg < fd->grid_e ? nwg : fd->grid_e);
+        hipLaunchKernelGGL(ke, dim3(ge), dim3(64 * EW), lds_emf(fd), st, (const uint32_t *)d_data, geo, tab, wk,
+                           (uint8_t *)d_out, cap);
+        FS_OK(hipGetLastError());
+    }
+    FS_OK(hipEventRecord(ev[3], st));
+    FS_OK(hipMemcpyAsync(h_flags, wk.flags, 64, hipMemcpyDeviceToHost, st));
+    FS_OK(hipStreamSynchronize(st));
+    const uint32_t fl = h_flags[0];
+    *total = (uint64_t)h_flags[2] | ((uint64_t)h_flags[3] << 32);
+    *leave = h_flags[4];
+    *entry = h_flags[5];
+    if (emit_from >= nt) *total = 0;
+    (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
+    (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
+    (void)hipEventElapsedTime(&ms[2], ev[2], ev[3]);
+    if (fl & FF_FAIL) return HH_ERR_UNSUPPORTED;
+    if (*total > cap || (fl & FF_OVER)) return HH_ERR_CAPACITY;
+    return HH_OK;
+}
+
+// Diagnostic: the count pass's arrays of the last decode (tests, tools).
+int fsm_debug_arrays(const FsmWs *ws, uint64_t nt, uint32_t *rec, uint32_t *fx, int32_t *tsum, uint32_t *xs) {
+    if (!ws->p) return HH_ERR_ARG;
+    const size_t o_rec = 64, o_tsum = o_rec + nt * NR * 4, o_xs = o_tsum + nt * 4, o_fx = o_xs + nt * 4;
+    const uint8_t *w = (const uint8_t *)ws->p;
+    if (o_fx + (nt + 1) * FX_W * 4 > ws->size) return HH_ERR_ARG;
+    FS_OK(hipDeviceSynchronize());
+    if (rec) FS_OK(hipMemcpy(rec, w + o_rec, nt * NR * 4, hipMemcpyDeviceToHost));
+    if (tsum) FS_OK(hipMemcpy(tsum, w + o_tsum, nt * 4, hipMemcpyDeviceToHost));
+    if (xs) FS_OK(hipMemcpy(xs, w + o_xs, nt * 4, hipMemcpyDeviceToHost));
+    if (fx) FS_OK(hipMemcpy(fx, w + o_fx, (nt + 1) * FX_W * 4, hipMemcpyDeviceToHost));
+    return HH_OK;
+}

@@ -1,0 +1,43 @@
+// hh_fsm_dev.h -- host interface of the state-machine decode kernels
+// (hh_fsm.hip), used by the decoder's host side (hh_device.hip).  C++ only,
+// not part of the public ABI.
+#ifndef HH_FSM_DEV_H_
+#define HH_FSM_DEV_H_
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hh_fsm.h"
+
+// Device copies of a tree's state-machine tables (hh_fsm_tables) and the
+// launch shapes that go with them.
+struct FsmDev {
+    uint32_t ok;             // tables built and uploaded
+    uint32_t ns, K, r, S, G;
+    uint16_t *ct;
+    uint32_t *b1;
+    uint8_t *tsym;
+    uint64_t *et, *er;
+    // persistent grids (workgroups), sized by the occupancy API for S / ns
+    uint32_t grid_c, grid_e, sized_S, sized_ns;
+};
+
+// One decode of tiles [0, ntiles) of the segment at d_data (bits readable
+// stream bits), the first `emit_from` a prologue, tile 0 entered in state
+// in_state.  Outputs: *total symbols written to d_out, *leave (state after
+// the last tile), *entry (state entering tile emit_from).  ms[0..2]: count,
+// scan, emission device time.  Returns HH_OK, HH_ERR_CAPACITY, HH_ERR_DEVICE,
+// HH_ERR_NOMEM or HH_ERR_UNSUPPORTED (chains that did not meet within
+// HH_FSM_KM regions: a code that does not resynchronise).
+struct FsmWs {
+    void *p;
+    size_t size;
+};
+int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
+               uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
+               hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms);
+int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G);
+void fsm_free(FsmDev *fd);
+int fsm_debug_arrays(const FsmWs *ws, uint64_t nt, uint32_t *rec, uint32_t *fx, int32_t *tsum, uint32_t *xs);
+
+#endif

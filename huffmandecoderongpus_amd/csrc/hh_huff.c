@@ -10,6 +10,7 @@
  */
 #include "hiphuff.h"
 #include "hh_internal.h"
+#include "hh_fsm.h"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -422,4 +423,78 @@ int hh_tables_build(const void *tree_v, hh_tables *T) {
         }
     }
     return HH_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* decode state machine (layout in hh_fsm.h)                           */
+/* ------------------------------------------------------------------ */
+/* One step of `nb` stream bits v (first bit in bit 0) from the internal node
+ * `node`: the node reached, the symbols completed (up to `cap` kept, first in
+ * bits 0..7) and their number. */
+static uint32_t fsm_walk(const hh_tables *T, uint32_t node, uint32_t v, unsigned nb, unsigned cap,
+                         uint32_t *syms, uint32_t *nsym) {
+    uint32_t s = 0, n = 0;
+    for (unsigned i = 0; i < nb; i++) {
+        node = tchild(T, node, (v >> i) & 1u);
+        if (tleaf(T, node)) {
+            if (n < cap) s |= (uint32_t)T->tsym[node] << (8 * n);
+            n++;
+            node = 0;
+        }
+    }
+    *syms = s;
+    *nsym = n;
+    return node;
+}
+
+int hh_fsm_build(const void *tv, uint32_t S, hh_fsm_tables *F) {
+    const hh_tables *T = (const hh_tables *)tv;
+    /* states: the internal nodes, in compact (BFS) order, root = 0 */
+    int32_t *st = (int32_t *)malloc(sizeof(int32_t) * T->tree_used);
+    uint32_t *node = (uint32_t *)malloc(sizeof(uint32_t) * (HH_FSM_MAXS + 1));
+    if (!st || !node) { free(st); free(node); return HH_ERR_NOMEM; }
+    uint32_t ns = 0;
+    int rc = HH_OK;
+    for (uint32_t i = 0; i < T->tree_used; i++) {
+        st[i] = -1;
+        if (!tleaf(T, i)) {
+            if (ns >= HH_FSM_MAXS) { rc = HH_ERR_UNSUPPORTED; goto out; }
+            st[i] = (int32_t)ns;
+            node[ns++] = i;
+        }
+    }
+    if (ns == 0 || st[0] != 0) { rc = HH_ERR_UNSUPPORTED; goto out; }
+    memset(F, 0, sizeof(*F));
+    F->ns = ns;
+    F->K = T->minlen >= 2 ? 6u : 4u;
+    F->S = S;
+    F->r = S % F->K;
+    for (uint32_t s = 0; s < ns; s++) {
+        const uint32_t nd = node[s];
+        F->tsym[s] = T->tsym[nd];
+        uint32_t sy, n;
+        for (uint32_t v = 0; v < 256; v++) {
+            const uint32_t to = fsm_walk(T, nd, v, 8, 0, &sy, &n);
+            F->ct[s * 256 + v] = (uint16_t)((uint32_t)st[to] | (n << 8));
+        }
+        for (uint32_t bit = 0; bit < 2; bit++) {
+            const uint32_t to = fsm_walk(T, nd, bit, 1, 1, &sy, &n);
+            F->b1[s * 2 + bit] = (uint32_t)st[to] | (n << 8) | (sy << 16);
+        }
+        const uint32_t K = F->K;
+        for (uint32_t v = 0; v < (1u << K); v++) {
+            const uint32_t to = fsm_walk(T, nd, v, K, 4, &sy, &n);
+            F->et[(s << K) | v] = (uint64_t)sy | ((uint64_t)((uint32_t)st[to] << (K + 3)) << 32) |
+                                  ((uint64_t)n << 56);
+        }
+        for (uint32_t v = 0; F->r && v < (1u << F->r); v++) {
+            const uint32_t to = fsm_walk(T, nd, v, F->r, 4, &sy, &n);
+            F->er[(s << F->r) | v] = (uint64_t)sy | ((uint64_t)((uint32_t)st[to] << (K + 3)) << 32) |
+                                     ((uint64_t)n << 56);
+        }
+    }
+out:
+    free(st);
+    free(node);
+    return rc;
 }

@@ -137,6 +137,10 @@ typedef struct {
                                    every code L <= 8 bits, e.g. E.coli's) is
                                    unpacked directly (k_fixed) unless this is
                                    set: then it takes the general pipeline */
+#define HH_FLAG_LEGACY 8        /* decode with round 2's pipeline (k_front,
+                                   k_walk, k_table, k_scan, k_emit) instead of
+                                   the state-machine decode (k_cnt, k_fscan,
+                                   k_emf) */
 
 int hh_decoder_create(hh_decoder **dec, const hh_config *cfg);
 void hh_decoder_destroy(hh_decoder *dec);
@@ -162,6 +166,8 @@ typedef struct {
                                 that does not resynchronise)                */
     int fixed_length;        /* 1: a complete fixed-length code, unpacked
                                 by k_fixed (HH_FLAG_NO_FIXED: 0)            */
+    int state_machine;       /* 1: the state-machine decode ran (k_cnt,
+                                k_fscan, k_emf)                             */
 } hh_stats;
 
 int hh_decoder_stats(const hh_decoder *dec, hh_stats *st);

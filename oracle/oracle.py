@@ -198,9 +198,27 @@ class RefHuff:
             raise ValueError(path)
 
     def __del__(self):
-        if getattr(self, "cd", None) and _REF is not None:
+        if getattr(self, "cd", None) and _REF is not None and getattr(self, "_owned", True):
             _REF.freeCompressedData(self.cd)
-            self.cd = None
+        self.cd = None
+
+    @classmethod
+    def from_arrays(cls, izero, ione, sym, data, bits: int, uncompressedsize: int = 0) -> "RefHuff":
+        """An in-memory CompressedData (huffdata.h:26-32) for the reference's
+        decoders: the tree as its HuffNode array, the payload followed by the
+        3 zero bytes loadHuffFile appends (huffdata.c:55-64)."""
+        self = cls.__new__(cls)
+        n = len(izero)
+        self._nodes = (_RefNode * n)(*[_RefNode(int(sym[i]) & 255, int(izero[i]), int(ione[i])) for i in range(n)])
+        nb = (bits + 7) // 8
+        self._data = np.zeros(nb + 3, dtype=np.uint8)
+        self._data[:nb] = np.asarray(data, np.uint8)[:nb]
+        self._cd = _RefCD(int(bits), n, int(uncompressedsize or bits),
+                          C.cast(self._nodes, C.POINTER(_RefNode)),
+                          self._data.ctypes.data_as(C.POINTER(C.c_ubyte)))
+        self.cd = C.pointer(self._cd)
+        self._owned = False
+        return self
 
     @property
     def uncompressedsize(self) -> int:

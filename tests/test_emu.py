@@ -171,3 +171,159 @@ def test_non_synchronising_code_is_detected(emu):
     n, out, st = run_emu(emu, iz, io, sy, data, bits, 0)
     assert st[3] == 352
     assert n == len(ref) and np.array_equal(out, ref)
+
+
+# ---------------------------------------------------------------------------
+# The state-machine decode (round 3's main path, hh_fsm.hip), emulated tile
+# by tile with the kernels' tables and per-lane rules (tests/emu/hh_fsm_emu.cpp)
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def femu():
+    if not os.path.exists(EMU):
+        pytest.skip("tests/emu/libhh_emu.so not built (make emu)")
+    L = C.CDLL(EMU)
+    L.hh_fsm_emu_decode.restype = C.c_int64
+    L.hh_fsm_emu_decode.argtypes = [C.c_void_p] * 3 + [C.c_int32, C.c_void_p, C.c_uint64, C.c_uint32,
+                                                       C.c_int32, C.c_uint64, C.c_uint64, C.c_uint32,
+                                                       C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                                       C.c_void_p]
+    L.hh_fsm_emu_tables.restype = C.c_int64
+    L.hh_fsm_emu_tables.argtypes = [C.c_void_p] * 3 + [C.c_int32, C.c_uint32, C.c_void_p]
+    return L
+
+
+def run_femu(L, izero, ione, sym, data, bits, S=0, G=-1, ntiles=0, prologue=0, in_state=0):
+    iz = np.ascontiguousarray(izero, np.int32)
+    io = np.ascontiguousarray(ione, np.int32)
+    sy = np.ascontiguousarray(sym, np.uint8)
+    d = np.zeros((bits + 7) // 8 + 64, np.uint8)
+    d[: (bits + 7) // 8] = np.asarray(data, np.uint8)[: (bits + 7) // 8]
+    out = np.zeros(bits + 16, np.uint8)
+    st = np.zeros(9, np.int64)
+    lv, en = C.c_uint32(), C.c_uint32()
+    n = L.hh_fsm_emu_decode(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), d.ctypes.data, bits, S, G,
+                            ntiles, prologue, in_state, out.ctypes.data, len(out), st.ctypes.data,
+                            C.byref(lv), C.byref(en))
+    return n, out[: max(n, 0)], st, lv.value, en.value
+
+
+@pytest.mark.parametrize("name", ["hello", "paper1", "news", "book2", "kjv.txt", "E.coli",
+                                  "world192.txt", "bible.txt"])
+@pytest.mark.parametrize("S", [0, 96])
+def test_fsm_fixtures(femu, name, S):
+    hf = H.HuffFile.load(os.path.join(FILES, name + ".huff"))
+    ref = O.OracleHuff.load(os.path.join(FILES, name + ".huff")).chain_decode()
+    n, out, st, _, _ = run_femu(femu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits, S)
+    assert n == len(ref) and np.array_equal(out, ref), (n, st)
+
+
+def test_fsm_walks_that_meet_late_are_exact(femu):
+    """Small regions and heads make guesses miss often and walks run past
+    their region (the rounds of walks, the next tile's corrections over
+    several regions): kjv.txt with 64-bit regions and 8-bit heads."""
+    hf = H.HuffFile.load(os.path.join(FILES, "kjv.txt.huff"))
+    ref = O.OracleHuff.load(os.path.join(FILES, "kjv.txt.huff")).chain_decode()
+    n, out, st, _, _ = run_femu(femu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits, 64, 8)
+    assert n == len(ref) and np.array_equal(out, ref)
+    assert st[2] > 0 and st[6] > 0           # walks past their region; multi-region corrections
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fsm_random_trees_and_tails(femu, seed):
+    rng = np.random.default_rng(seed)
+    nleaves = int(rng.integers(2, 120))
+    iz, io, sy, syms = random_tree(rng, nleaves)
+    t = H.Tree(iz, io, sy)
+    if t.info()["maxlen"] > 64:
+        pytest.skip("encoder limit")
+    p = rng.dirichlet(np.full(nleaves, 0.3))
+    text = rng.choice(syms, size=int(rng.integers(1, 60000)), p=p).astype(np.uint8)
+    data, bits = t.encode(text)
+    for cut in (bits, bits - 1, max(1, bits // 3 + 1)):   # cut codes exercise the tail rule
+        ref = oracle_chain(iz, io, sy, data, cut)
+        for S in (0, 64):
+            n, out, st, _, _ = run_femu(femu, iz, io, sy, data, cut, S)
+            if n == UNSUPPORTED:       # a code whose chains never meet (lattice)
+                continue
+            assert n == len(ref) and np.array_equal(out, ref), (cut, S, st)
+
+
+def test_fsm_long_codes(femu):
+    """Codes of up to 40 bits (a skewed tree): the state machine has no code
+    length limit (round 2's fast path stopped at 32 bits)."""
+    iz, io, sy = [-1], [-1], [0]
+    v = 0
+    for depth in range(40):                  # a caterpillar: code lengths 1..40
+        a, b = len(iz), len(iz) + 1
+        iz[v], io[v] = a, b
+        iz += [-1, -1]; io += [-1, -1]; sy += [depth & 255, (depth + 100) & 255]
+        v = b
+    iz, io, sy = np.array(iz), np.array(io), np.array(sy)
+    t = H.Tree(iz, io, sy)
+    assert t.info()["maxlen"] == 40
+    rng = np.random.default_rng(7)
+    leaves = [i for i in range(len(iz)) if iz[i] == -1]
+    text = sy[rng.choice(leaves, size=20000, p=np.full(len(leaves), 1 / len(leaves)))].astype(np.uint8)
+    data, bits = t.encode(text)
+    ref = oracle_chain(iz, io, sy, data, bits)
+    n, out, st, _, _ = run_femu(femu, iz, io, sy, data, bits)
+    assert n == len(ref) and np.array_equal(out, ref)
+
+
+def test_fsm_segments_concatenate(femu):
+    """Segments (multi-GPU shards): tiles [a, b) decoded with PROBE tiles of
+    the predecessor as a prologue; each entry equals the predecessor's leave
+    state and the outputs concatenate to the stream."""
+    hf = H.HuffFile.load(os.path.join(FILES, "kjv.txt.huff"))
+    ref = O.OracleHuff.load(os.path.join(FILES, "kjv.txt.huff")).chain_decode()
+    n, _, st, _, _ = run_femu(femu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits)
+    tb = 64 * int(st[3])
+    nt = (hf.bits + tb - 1) // tb
+    cuts = [0, nt // 5, nt // 2, nt - 3, nt]
+    parts, prev_leave = [], 0
+    payload = np.asarray(hf.payload, np.uint8)
+    for a, b in zip(cuts, cuts[1:]):
+        pro = min(2, a)
+        start = (a - pro) * tb
+        sub = payload[start // 8:]
+        bits = min(hf.bits - start, (b - a + pro + 1) * tb)
+        m, out, _, leave, entry = run_femu(femu, hf.izero, hf.ione, hf.sym, sub, bits, ntiles=b - a + pro,
+                                           prologue=pro)
+        assert m >= 0
+        assert entry == prev_leave          # the prologue found the true entry state
+        parts.append(out)
+        prev_leave = leave
+    got = np.concatenate(parts)
+    assert len(got) == len(ref) and np.array_equal(got, ref)
+
+
+def test_fsm_fixed_length_codes(femu):
+    """Fixed-length codes: regions on the code lattice need no head (the root
+    is always right); off the lattice (S not a multiple of L) chains never
+    meet and the decode reports it (-> the segment path), never a wrong
+    answer."""
+    for L_, S in ((5, 0), (3, 0), (5, 256)):
+        iz, io, sy = complete_tree(L_)
+        rng = np.random.default_rng(L_)
+        bits = L_ * 30000
+        data = rng.integers(0, 256, size=bits // 8 + 1).astype(np.uint8)
+        ref = oracle_chain(iz, io, sy, data, bits)
+        n, out, st, _, _ = run_femu(femu, iz, io, sy, data, bits, S)
+        if S and S % L_:
+            assert n == UNSUPPORTED
+        else:
+            assert st[4] == 0 and st[1] == 0     # no head, no walks
+            assert n == len(ref) and np.array_equal(out, ref)
+
+
+def test_fsm_tables_shape(femu):
+    """State machine sizes of the fixtures: emission steps of 6 bits for codes
+    of >= 2 bits, a 4-bit remainder step for 256-bit regions."""
+    hf = H.HuffFile.load(os.path.join(FILES, "kjv.txt.huff"))
+    info = np.zeros(4, np.uint32)
+    iz = np.ascontiguousarray(hf.izero, np.int32)
+    io = np.ascontiguousarray(hf.ione, np.int32)
+    sy = np.ascontiguousarray(hf.sym, np.uint8)
+    assert femu.hh_fsm_emu_tables(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), 256,
+                                  info.ctypes.data) == 0
+    assert list(info) == [83, 6, 4, 64]
