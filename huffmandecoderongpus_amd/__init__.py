@@ -262,9 +262,15 @@ class Decoder:
         _check(lib().hh_decoder_stats(self._h, C.byref(st)), "stats")
         return {k: getattr(st, k) for k, _ in _Stats._fields_}
 
-    def decode_host(self, payload: np.ndarray, bits: int, cap: int) -> np.ndarray:
+    def decode_host(self, payload: np.ndarray, bits: int, cap: int,
+                    out: Optional[np.ndarray] = None) -> np.ndarray:
+        """The evaluate() scope: host payload in, host symbols out.  `out`
+        (uint8, >= cap) may be the caller's buffer, allocated and touched
+        beforehand as evaluate() does (decodeUtil.c:37-38, 55)."""
         payload = np.ascontiguousarray(payload, np.uint8)
-        out = np.zeros(max(cap, 1), np.uint8)
+        if out is None:
+            out = np.zeros(max(cap, 1), np.uint8)
+        assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= cap
         n = C.c_uint64(0)
         _check(lib().hh_decode_host(self._h, payload.ctypes.data, bits, out.ctypes.data, cap,
                                     C.byref(n)), "decode_host")

@@ -1408,6 +1408,10 @@ struct hh_decoder {
     hh_fsm_tables *ft;
     FsmDev fsm;
     FsmWs fsm_ws;
+    // evaluate() scope pipeline (host_pipeline): copy streams, per-chunk events
+    hipStream_t h2d, d2h;
+    hipEvent_t *pipe_ev;
+    uint32_t npipe_ev;
 };
 
 static int ensure_dev(void **p, size_t *have, size_t need) {
@@ -1487,6 +1491,10 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
     if (d->stream) hipStreamDestroy(d->stream);
     fsm_free(&d->fsm);
     if (d->fsm_ws.p) hipFree(d->fsm_ws.p);
+    for (uint32_t i = 0; i < d->npipe_ev; i++) hipEventDestroy(d->pipe_ev[i]);
+    free(d->pipe_ev);
+    if (d->h2d) hipStreamDestroy(d->h2d);
+    if (d->d2h) hipStreamDestroy(d->d2h);
     free(d->ht);
     free(d->ft);
     free(d);
@@ -2045,7 +2053,10 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
     memset(&d->stats, 0, sizeof(d->stats));
     memset(ro, 0, sizeof(*ro));
     ro->leave_state = ro->entry_state = rg->in_state;
-    if (rg->bits_avail == 0) return HH_OK;
+    // no tiles (a shard with none of its own when there are fewer tiles than
+    // ranks): nothing written, the chain leaves in the state it entered
+    ro->entry_exact = rg->prologue == 0;
+    if (rg->bits_avail == 0 || rg->ntiles == 0) return HH_OK;
     if (fsm_path_ok(d)) {
         // states are state-machine states (0: the root, the stream start)
         if (rg->in_state >= d->fsm.ns) return HH_ERR_ARG;
@@ -2128,6 +2139,89 @@ static int host_pipe(hh_decoder *d, uint8_t *host, uint8_t *dev, size_t n, bool 
     return HH_OK;
 }
 
+// The evaluate() scope, pipelined (state-machine path): the caller's buffers
+// are page-locked for the call (hipHostRegister) so that the DMA engines read
+// and write them directly; the payload goes up in chunks of whole tiles on
+// one copy stream, chunk k is decoded as a segment as soon as it has landed
+// (entered in the state chunk k-1 left), and its symbols go down on a second
+// copy stream while later chunks are still uploading and decoding.
+#define HH_PIPE_CHUNK ((uint64_t)128 << 20)          // payload bytes per chunk
+
+static uint64_t pipe_chunk() {
+    const char *e = getenv("HH_PIPE_CHUNK_KB");        // (tests: force many chunks)
+    const uint64_t v = e ? strtoull(e, nullptr, 10) << 10 : 0;
+    return v ? v : HH_PIPE_CHUNK;
+}
+
+static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint8_t *out, uint64_t cap,
+                         uint64_t *out_len) {
+    const uint64_t nb = (bits + 7) / 8;
+    const uint64_t tbb = (uint64_t)HH_NR * d->S / 8;                 // bytes per tile
+    const uint64_t ch = pipe_chunk() > tbb ? pipe_chunk() / tbb * tbb : tbb;
+    const uint64_t nch = (nb + ch - 1) / ch;
+    if (!d->h2d) {
+        HIP_OK(hipStreamCreateWithFlags(&d->h2d, hipStreamNonBlocking));
+        HIP_OK(hipStreamCreateWithFlags(&d->d2h, hipStreamNonBlocking));
+    }
+    if (nch > d->npipe_ev) {
+        for (uint32_t i = 0; i < d->npipe_ev; i++) (void)hipEventDestroy(d->pipe_ev[i]);
+        free(d->pipe_ev);
+        d->npipe_ev = 0;
+        d->pipe_ev = (hipEvent_t *)calloc(nch, sizeof(hipEvent_t));
+        if (!d->pipe_ev) return HH_ERR_NOMEM;
+        for (uint64_t i = 0; i < nch; i++) {
+            HIP_OK(hipEventCreateWithFlags(&d->pipe_ev[i], hipEventDisableTiming));
+            d->npipe_ev = (uint32_t)(i + 1);
+        }
+    }
+    if (hipHostRegister((void *)data, nb, hipHostRegisterDefault) != hipSuccess) return HH_ERR_UNSUPPORTED;
+    if (cap && hipHostRegister(out, cap, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipHostUnregister((void *)data);
+        return HH_ERR_UNSUPPORTED;
+    }
+    int rc = HH_OK;
+    uint8_t *din = (uint8_t *)d->d_in, *dout = (uint8_t *)d->d_out;
+    if (hipMemsetAsync(din + nb, 0, HH_PAYLOAD_PAD, d->h2d) != hipSuccess) rc = HH_ERR_DEVICE;
+    for (uint64_t k = 0; k < nch && !rc; k++) {
+        const uint64_t o = k * ch, len = nb - o < ch ? nb - o : ch;
+        if (hipMemcpyAsync(din + o, data + o, len, hipMemcpyHostToDevice, d->h2d) != hipSuccess ||
+            hipEventRecord(d->pipe_ev[k], d->h2d) != hipSuccess)
+            rc = HH_ERR_DEVICE;
+    }
+    uint64_t total = 0;
+    uint32_t state = 0;
+    float ms_all[3] = {0, 0, 0};
+    for (uint64_t k = 0; k < nch && !rc; k++) {
+        const uint64_t b0 = k * ch * 8;
+        const uint64_t ntiles = (k + 1 < nch ? ch * 8 : bits - b0 + d->S * HH_NR - 1) / (d->S * HH_NR);
+        // readable bits: the chunk and the first tile of the next (the stream
+        // end lies beyond a chunk's tiles, except in the last one)
+        const uint64_t avail = bits - b0 < (ch + tbb) * 8 ? bits - b0 : (ch + tbb) * 8;
+        if (hipStreamWaitEvent(d->stream, d->pipe_ev[k], 0) != hipSuccess) { rc = HH_ERR_DEVICE; break; }
+        // (the first tile of the next chunk may not have landed yet: the
+        // kernels read it only for chains that this segment does not use)
+        uint64_t n = 0;
+        uint32_t leave = 0, en = 0;
+        float ms[3] = {0, 0, 0};
+        rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, din + k * ch, avail, ntiles, state, 0,
+                        dout + total, cap - total, d->stream, &n, &leave, &en, ms);
+        if (rc) break;
+        for (int i = 0; i < 3; i++) ms_all[i] += ms[i];
+        if (n && hipMemcpyAsync(out + total, dout + total, n, hipMemcpyDeviceToHost, d->d2h) != hipSuccess) {
+            rc = HH_ERR_DEVICE;
+            break;
+        }
+        total += n;
+        state = leave;
+    }
+    if (hipStreamSynchronize(d->d2h) != hipSuccess || hipStreamSynchronize(d->h2d) != hipSuccess) rc = rc ? rc : HH_ERR_DEVICE;
+    (void)hipHostUnregister((void *)data);
+    if (cap) (void)hipHostUnregister(out);
+    fsm_stats(d, bits, total, ms_all);
+    *out_len = total;
+    return rc;
+}
+
 extern "C" int hh_decode_host(hh_decoder *d, const uint8_t *data, uint64_t bits, uint8_t *out,
                               uint64_t cap, uint64_t *out_len) {
     if (!d || !out_len || (!data && bits) || (!out && cap)) return HH_ERR_ARG;
@@ -2146,6 +2240,11 @@ extern "C" int hh_decode_host(hh_decoder *d, const uint8_t *data, uint64_t bits,
         if (hipEventCreateWithFlags(&d->h_ev[0], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&d->h_ev[1], hipEventDisableTiming) != hipSuccess)
             return HH_ERR_DEVICE;
+    }
+    if (fsm_path_ok(d) && nb > pipe_chunk() && !getenv("HH_HOST_SERIAL")) {
+        rc = host_pipeline(d, data, bits, out, cap, out_len);
+        if (rc != HH_ERR_UNSUPPORTED) return rc;   // (unsupported: registration refused -> staged copies)
+        rc = HH_OK;
     }
     HIP_OK(hipMemsetAsync((uint8_t *)d->d_in + nb, 0, HH_PAYLOAD_PAD, d->stream));
     rc = host_pipe(d, (uint8_t *)data, (uint8_t *)d->d_in, nb, true);

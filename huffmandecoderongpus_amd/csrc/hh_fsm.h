@@ -15,12 +15,15 @@
  * pointer doubling, makebigtable.cl:10-40).
  *
  * States are numbered 0..ns-1 (internal nodes of the compact tree, BFS
- * order, root first); ns <= HH_FSM_MAXS keeps a state in 8 bits.
+ * order, root first); ns <= HH_FSM_MAXS keeps a state's table row (state
+ * << 9 bytes) in 16 bits.
  *
  *   ct[s * 256 + b]   u16: 8-bit steps (count pass): the state after the 8
  *                     stream bits b (stream bit p in bit 0, the reference's
- *                     LSB-first order, decodeallbits.cl:23) | the codes
- *                     completed on the way << 8
+ *                     LSB-first order, decodeallbits.cl:23) << 9, i.e. its
+ *                     row's byte offset | the codes completed on the way
+ *                     (bits 0..3): the next lookup's address is
+ *                     (entry & 0xfe00) | b << 1
  *   b1[s * 2 + bit]   u32: 1-bit steps (the stream's last partial byte):
  *                     next state | completed << 8 | the symbol << 16
  *   tsym[s]           the sym byte of the state's node: the symbol the
@@ -29,9 +32,13 @@
  *   et[s << K | v]    u64: K-bit steps (emission), v = the next K bits
  *       bits  0..31   the symbols completed (first in bits 0..7, unused
  *                     bytes 0): K = 6 for codes of >= 2 bits (<= 3
- *                     symbols), K = 4 when a code has 1 bit (<= 4)
- *       bits 32..55   the next state's row in et, in bytes: next << (K + 3)
- *       bits 56..58   the number of symbols
+ *                     symbols, bits 24..31 then 0), K = 4 when a code has
+ *                     1 bit (<= 4)
+ *       bits 32..36   (32 - 8 x the number of symbols) mod 32: the rotation
+ *                     that moves the K = 6 kernel's output position (a
+ *                     one-hot multiplier) on
+ *       bits 40..47   8 x the number of symbols
+ *       bits 48..63   the next state's row in et, in bytes: next << (K + 3)
  *   er[s << r | v]    u64: the r-bit step that ends a region of S bits when K
  *                     does not divide S (r = S mod K, 0: none); same layout,
  *                     rows in et units
@@ -41,7 +48,7 @@
 
 #include <stdint.h>
 
-#define HH_FSM_MAXS 255
+#define HH_FSM_MAXS 127
 
 typedef struct {
     uint32_t ns;              /* states (internal nodes)                      */
@@ -56,8 +63,13 @@ typedef struct {
 } hh_fsm_tables;
 
 #define HH_FSM_ET_SYMS(e) ((uint32_t)(e))
-#define HH_FSM_ET_ROW(e) ((uint32_t)((e) >> 32) & 0xffffffu)
-#define HH_FSM_ET_NSYM(e) ((uint32_t)((e) >> 56) & 7u)
+#define HH_FSM_ET_ROW(e) ((uint32_t)((e) >> 48))
+#define HH_FSM_ET_NSYM(e) ((uint32_t)((e) >> 43) & 31u)
+#define HH_FSM_ET_MAKE(syms, row, n)                                                    \
+    ((uint64_t)(uint32_t)(syms) | (uint64_t)((32u - 8u * (uint32_t)(n)) & 31u) << 32 | \
+     (uint64_t)(8u * (uint32_t)(n)) << 40 | (uint64_t)(uint32_t)(row) << 48)
+#define HH_FSM_CT_NEXT(v) ((uint32_t)(v) >> 9)
+#define HH_FSM_CT_CNT(v) ((uint32_t)(v) & 15u)
 
 #ifdef __cplusplus
 extern "C" {

@@ -28,6 +28,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "hh_fsm_algo.h"
 #include "hh_fsm_dev.h"
 #include "hiphuff.h"
@@ -99,6 +101,13 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
     return v;
 }
 __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1, 64); }
+// a wave-uniform 64-bit value in scalar registers (the compiler cannot always
+// tell; a buffer resource built from a vector value costs a waterfall loop)
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+    return (uint64_t)hi << 32 | lo;
+}
 
 #define WAVE_SYNC()                                                    \
     do {                                                               \
@@ -140,6 +149,16 @@ __device__ __forceinline__ uint32_t rbits(const uint32_t *w, uint32_t q, uint32_
     if (o + n <= 32 || i + 1 >= SW) return __builtin_amdgcn_ubfe(w[i], o, n);
     return __builtin_amdgcn_alignbit(w[i + 1], w[i], o) & ((1u << n) - 1u);
 }
+// bits [q, q+K) of a region times 8: a byte offset into a row of the
+// emission table (compile-time q)
+template <uint32_t SW, uint32_t K>
+__device__ __forceinline__ uint32_t win8(const uint32_t *w, uint32_t q) {
+    constexpr uint32_t M = ((1u << K) - 1u) << 3;
+    if (q < 3) return (w[0] << (3 - q)) & M;
+    const uint32_t p = q - 3, i = p >> 5, o = p & 31;
+    if (o + K + 3 <= 32 || i + 1 >= SW) return (w[i] >> o) & M;
+    return __builtin_amdgcn_alignbit(w[i + 1], w[i], o) & M;
+}
 // bit q of a region held in registers, q not a compile-time constant (rare paths)
 template <uint32_t SW>
 __device__ __forceinline__ uint32_t rbit_dyn(const uint32_t *w, uint32_t q) {
@@ -149,16 +168,23 @@ __device__ __forceinline__ uint32_t rbit_dyn(const uint32_t *w, uint32_t q) {
     return (x >> (q & 31)) & 1u;
 }
 
-// count table: next state | completed << 8, at LDS address 0
-__device__ __forceinline__ uint32_t ct_at(const uint8_t *lds, uint32_t s, uint32_t b) {
-    return *(const uint16_t *)(lds + ((s << 9) | (b << 1)));
+// The count table at LDS address 0: a state is carried as its row's byte
+// offset (state << 9), an entry is the next row | the codes completed, so
+// the next lookup's address is one AND-OR of the entry and the byte.
+__device__ __forceinline__ uint32_t ct_at(const uint8_t *lds, uint32_t row, uint32_t b) {
+    return *(const uint16_t *)(lds + ((row & 0xfe00u) | (b << 1)));
+}
+__device__ __forceinline__ uint32_t b1_row(const uint32_t *b1, uint32_t row, uint32_t bit, uint32_t *c) {
+    const uint32_t v = b1[(row >> 9) * 2 + bit];
+    *c += (v >> 8) & 255u;
+    return (v & 255u) << 9;
 }
 
 // ---------------------------------------------------------------------------
-// Region passes of k_cnt on words in registers.  lim: the region's readable
-// bits (S unless the stream ends inside it); TAIL instantiations check it.
+// Region passes of k_cnt on words in registers (states as rows).  lim: the
+// region's readable bits (S unless the stream ends inside it); only the TAIL
+// instantiations check it.
 // ---------------------------------------------------------------------------
-// Count of a region entered in state s; returns the exit state.
 template <uint32_t SW, bool TAIL>
 __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
                                                uint32_t s, uint32_t lim, uint32_t *n) {
@@ -167,24 +193,20 @@ __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_
     for (uint32_t k = 0; k < 4 * SW; k++) {
         if (!TAIL || 8 * k + 8 <= lim) {
             const uint32_t e = ct_at(lds, s, rbyte<SW>(w, k));
-            s = e & 255u;
-            c += e >> 8;
+            s = e;
+            c += e & 15u;
         }
     }
-    if (TAIL) {
-        for (uint32_t q = lim & ~7u; q < lim; q++) {       // the last partial byte, bit by bit
-            const uint32_t e = b1[s * 2 + rbit_dyn<SW>(w, q)];
-            s = e & 255u;
-            c += (e >> 8) & 255u;
-        }
-    }
+    s &= 0xfe00u;
+    if (TAIL)
+        for (uint32_t q = lim & ~7u; q < lim; q++) s = b1_row(b1, s, rbit_dyn<SW>(w, q), &c);   // the last partial byte
     *n = c;
     return s;
 }
 
 // Walk: chains A and B stepped together over a region until they meet
 // (their count difference stops changing then); lanes not walking carry
-// A == B.  Returns 1 if every lane met; the caller checks A == B per lane.
+// A == B.  Stops when every lane has met.
 template <uint32_t SW, bool TAIL>
 __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
                                             uint32_t &A, uint32_t &B, int32_t &d, uint32_t lim) {
@@ -194,34 +216,34 @@ __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *
         if (go && (!TAIL || 8 * k + 8 <= lim)) {
             const uint32_t x = rbyte<SW>(w, k);
             const uint32_t ea = ct_at(lds, A, x), eb = ct_at(lds, B, x);
-            A = ea & 255u;
-            B = eb & 255u;
-            d += (int32_t)(ea >> 8) - (int32_t)(eb >> 8);
+            A = ea & 0xfe00u;
+            B = eb & 0xfe00u;
+            d += (int32_t)(ea & 15u) - (int32_t)(eb & 15u);
         }
         if ((k & 3) == 3 && go) go = __ballot(A != B) != 0;
     }
     if (TAIL) {
         for (uint32_t q = lim & ~7u; q < lim && A != B; q++) {
             const uint32_t x = rbit_dyn<SW>(w, q);
-            const uint32_t ea = b1[A * 2 + x], eb = b1[B * 2 + x];
-            A = ea & 255u;
-            B = eb & 255u;
-            d += (int32_t)((ea >> 8) & 255u) - (int32_t)((eb >> 8) & 255u);
+            uint32_t ca = 0, cb = 0;
+            A = b1_row(b1, A, x, &ca);
+            B = b1_row(b1, B, x, &cb);
+            d += (int32_t)ca - (int32_t)cb;
         }
     }
 }
 
 // ---------------------------------------------------------------------------
-// k_cnt: the count pass of every tile, one tile per wave.
+// k_cnt: the count pass of tiles [t0, t1), one tile per wave.  TAIL: the
+// tiles in which the stream ends (or whose next tile's region 0 holds the
+// end), launched on their own.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns) {
     return ((ns * 512u + ns * 8u + ns) + 15u) & ~15u;
 }
 
-
-// One tile of the count pass (TAIL: the stream ends in this tile or in the
-// next tile's first region).  w: region j's words, nx: region j+1's (lane 63:
-// the next tile's region 0).
+// One tile: w = region j's words, nx = region j+1's (lane 63: the next
+// tile's region 0).
 template <uint32_t SW, bool TAIL>
 __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
                                          const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
@@ -246,12 +268,19 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
 #pragma unroll
         for (uint32_t k = 4 * SW - 8; k < 4 * SW; k++) {
             gs = k == 4 * SW - GB ? 0u : gs;
-            gs = ct_at(lds, gs, rbyte<SW>(w, k)) & 255u;
+            gs = ct_at(lds, gs, rbyte<SW>(w, k));
         }
+        gs &= 0xfe00u;
     }
-    const uint32_t sp = j ? shfl_up1(gs) : (t == 0 ? geo.in_state : 0u);
+    const uint32_t gup = shfl_up1(gs);              // (cross-lane ops with every lane active)
+    const uint32_t sp = j ? gup : (t == 0 ? geo.in_state << 9 : 0u);
     uint32_t n;
     uint32_t X = cnt_region<SW, TAIL>(lds, F.b1, w, sp, lim, &n);   // region j's exit (given its entry)
+    // the stream ends in region j / in region j+1: the tail rule counts a
+    // chain that is not at the root there (fsm_region, fsm_walk2)
+    const bool endj = TAIL && lim > 0 && R + lim == geo.bits;
+    const bool endn = TAIL && limn > 0 && R + S + limn == geo.bits;
+    if (endj && X != 0) n += 1;
 
     // makebigtable: where region j's exit differs from the entry assumed for
     // region j+1 (E), lane j walks region j+1 with both chains; their count
@@ -267,13 +296,19 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
         if (__ballot(want) == 0) break;
         uint32_t A = X, B = want ? E : X;           // (not walking: A == B, no change)
         int32_t dd = 0;
-        walk_region<SW, TAIL>(lds, F.b1, nx, A, B, dd, limn);
+        uint32_t nv[SW];
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) {
+            nv[k] = nx[k];
+            asm volatile("" : "+v"(nv[k]));
+        }
+        walk_region<SW, TAIL>(lds, F.b1, nv, A, B, dd, limn);
         bool deep = false;
         if (want) {
-            if (TAIL && A != B && limn < S) dd += (int32_t)(A != 0) - (int32_t)(B != 0);   // tail rule
+            if (endn && A != B) dd += (int32_t)(A != 0) - (int32_t)(B != 0);   // tail rule
             d += dd;
             E = X;
-            deep = A != B && limn == S;
+            deep = A != B && !endn;
             if (j == 63 && deep) {
                 lost = true;
                 deep = false;
@@ -284,11 +319,12 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     }
 
     // records: region j entered in the state lane j-1 assumed last
-    const uint32_t ent = j ? shfl_up1(E) : sp;
-    const uint32_t cnt = (uint32_t)((int32_t)n + (j ? (int32_t)shfl_up1((uint32_t)d) : 0));
+    const uint32_t Eup = shfl_up1(E), dup = shfl_up1((uint32_t)d);
+    const uint32_t ent = (j ? Eup : sp) >> 9;
+    const uint32_t cnt = (uint32_t)((int32_t)n + (j ? (int32_t)dup : 0));
     wk.rec[t * NR + j] = fsm_rec(ent, cnt);
     const int32_t sum = wave_sum((int32_t)cnt);
-    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63);
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63) >> 9;
     if (j == 0) {
         wk.tsum[t] = sum;
         wk.xs[t] = x;
@@ -298,7 +334,7 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     if (has_next) {
         const bool lst = __builtin_amdgcn_readlane((int)lost, 63) != 0;
         if (!lst) {
-            const uint32_t E63 = (uint32_t)__builtin_amdgcn_readlane((int)E, 63);
+            const uint32_t E63 = (uint32_t)__builtin_amdgcn_readlane((int)E, 63) >> 9;
             const int32_t d63 = __builtin_amdgcn_readlane(d, 63);
             if (j < FX_W) wk.fx[(t + 1) * FX_W + j] = j == 0 && (E63 | (uint32_t)d63) ? fsm_fx(E63, d63) : 0u;
         } else if (j == 0) {
@@ -311,11 +347,13 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     }
 }
 
-template <uint32_t SW>
-__global__ __launch_bounds__(64 * CW) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk) {
+template <uint32_t SW, bool TAIL>
+__global__ __launch_bounds__(64 * CW) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+                                                 uint64_t t0, uint64_t t1) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW;
-    const uint32_t ns = geo.ns, tid = threadIdx.x, j = tid & 63u, wv = tid >> 6;
+    const uint32_t ns = geo.ns, tid = threadIdx.x, j = tid & 63u;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // (uniform: scalar tile index)
     uint32_t *s_b1 = (uint32_t *)(smem + ns * 512);
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
     for (uint32_t i = tid; i < ns * 128; i += blockDim.x) ((uint32_t *)smem)[i] = ((const uint32_t *)tab.ct)[i];
@@ -324,28 +362,25 @@ __global__ __launch_bounds__(64 * CW) void k_cnt(const uint32_t *__restrict__ g,
     __syncthreads();
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts};
     const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * CW;
-    // tiles whose regions (and the next tile's region 0) end before the stream
-    const uint64_t nfast = geo.bits >= TB + S ? (geo.bits - S) / TB : 0;
-    uint64_t t = (uint64_t)blockIdx.x * CW + wv;
+    uint64_t t = t0 + (uint64_t)blockIdx.x * CW + wv;
     // the next tile's words are loaded one tile ahead
     uint32_t pw[SW], pn[SW];
     auto prefetch = [&](uint64_t tt) {
+        tt = uni64(tt);
         const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
         fs_load<SW>(pw, rs, j * SW);
         fs_load<SW>(pn, rs, (j + 1) * SW);
     };
-    if (t < geo.ntiles) prefetch(t);
-    for (; t < geo.ntiles; t += nwv) {
+    if (t < t1) prefetch(t);
+    for (; t < t1; t += nwv) {
         uint32_t w[SW], nx[SW];
 #pragma unroll
         for (uint32_t k = 0; k < SW; k++) {
             w[k] = pw[k];
             nx[k] = pn[k];
         }
-        const uint64_t tn = t + nwv < geo.ntiles ? t + nwv : t;
-        prefetch(tn);
-        if (t < nfast) cnt_tile<SW, false>(smem, F, g, geo, wk, t, w, nx);
-        else cnt_tile<SW, true>(smem, F, g, geo, wk, t, w, nx);
+        prefetch(t + nwv < t1 ? t + nwv : t);
+        cnt_tile<SW, TAIL>(smem, F, g, geo, wk, t, w, nx);
     }
 }
 
@@ -417,7 +452,7 @@ __global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// k_emf: emission of every emitted tile, one tile per wave.
+// k_emf: emission of tiles [t0, t1), one tile per wave.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, uint32_t r) {
     return ((ns << K) * 8u + (r ? (ns << r) * 8u : 0u) + ns * 8u + ns + 15u) & ~15u;
@@ -430,7 +465,7 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
 // step; TAIL: steps while whole, the rest bit by bit, and the tail rule.
 // The unused bytes of every stored dword are zero: a dword shared with the
 // neighbouring runs is repaired by OR afterwards (emf_edges).  e4 receives
-// the first four steps' entries; *last the run's last dword value.
+// the first four steps' entries; *lastw / *lastwd the run's last dword.
 template <uint32_t SW, uint32_t K, bool TAIL>
 __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, uint32_t r, const uint32_t *b1,
                                            const uint8_t *ts, const uint32_t *w, uint32_t s, uint32_t lim,
@@ -439,15 +474,28 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, uint32
     constexpr uint32_t S = 32 * SW;
     uint32_t row = s << (K + 3);
     uint32_t wd = oa & ~3u, sh = (oa & 3u) * 8u;
-    uint64_t acc = 0;
+    uint32_t a = 0;                                 // the current dword's bytes so far
     auto put = [&](uint64_t e) {
-        acc |= (uint64_t)(uint32_t)e << sh;
-        *(uint32_t *)(lds + wd) = (uint32_t)acc;
-        sh += (uint32_t)(e >> 53) & 0x38u;          // 8 * nsym
-        const bool full = sh >= 32;
-        wd += full ? 4u : 0u;
-        acc = full ? acc >> 32 : acc;
-        sh &= 31u;
+        const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
+        const uint32_t u = sh + ((hi >> 8) & 255u);   // 8 x the symbols: one SDWA add
+        if (K == 6) {
+            // <= 3 symbol bytes: what does not fit the current dword spills
+            // into the next (nothing spills when sh = 0)
+            const uint32_t an = (lo << sh) | a;
+            const uint32_t sp = __builtin_amdgcn_alignbit(0u, lo, (0u - sh) & 31u);
+            *(uint32_t *)(lds + wd) = an;
+            const bool full = u >= 32;
+            a = full ? sp : an;
+            wd += full ? 4u : 0u;
+        } else {
+            // <= 4 bytes (1-bit codes): a 64-bit shift
+            const uint64_t acc = (uint64_t)a | ((uint64_t)lo << sh);
+            *(uint32_t *)(lds + wd) = (uint32_t)acc;
+            const bool full = u >= 32;
+            a = full ? (uint32_t)(acc >> 32) : (uint32_t)acc;
+            wd += full ? 4u : 0u;
+        }
+        sh = u & 31u;
     };
 #pragma unroll
     for (uint32_t i = 0; i < 4; i++) e4[i] = 0;
@@ -455,9 +503,9 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, uint32
     for (uint32_t k = 0; k < S / K; k++) {
         const uint32_t q = k * K;
         if (!TAIL || q + K <= lim) {
-            const uint64_t e = *(const uint64_t *)(lds + row + (rbits<SW>(w, q, K) << 3));
+            const uint64_t e = *(const uint64_t *)(lds + row + win8<SW, K>(w, q));
             put(e);
-            row = (uint32_t)(e >> 32) & 0xffffffu;
+            row = (uint32_t)(e >> 48);
             if (k < 4) e4[k] = e;
         }
     }
@@ -465,20 +513,20 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, uint32
         if (r) {
             const uint64_t e = *(const uint64_t *)(lds + er_off + (row >> (K - r)) + (rbits<SW>(w, S - r, r) << 3));
             put(e);
-            row = (uint32_t)(e >> 32) & 0xffffffu;
+            row = (uint32_t)(e >> 48);
         }
     } else {
         uint32_t st = row >> (K + 3);
         for (uint32_t q = lim / K * K; q < lim; q++) {
             const uint32_t v = b1[st * 2 + rbit_dyn<SW>(w, q)];
             st = v & 255u;
-            put((uint64_t)((v >> 16) & 255u) | ((uint64_t)((v >> 8) & 255u) << 56));
+            put(HH_FSM_ET_MAKE((v >> 16) & 255u, 0u, (v >> 8) & 255u));
         }
         row = st << (K + 3);
     }
-    if (at_end && (row >> (K + 3)) != 0) put((uint64_t)ts[row >> (K + 3)] | (1ull << 56));   // the tail rule
-    *(uint32_t *)(lds + wd) = (uint32_t)acc;        // the bytes of the last step's overflow
-    *lastw = (uint32_t)acc;
+    if (at_end && (row >> (K + 3)) != 0) put(HH_FSM_ET_MAKE(ts[row >> (K + 3)], 0u, 1u));   // the tail rule
+    *(uint32_t *)(lds + wd) = a;                     // the bytes of the last step's overflow
+    *lastw = a;
     *lastwd = wd;
 }
 
@@ -498,7 +546,7 @@ __device__ __forceinline__ void emf_edges(uint8_t *lds, const uint32_t *b1, cons
 #pragma unroll
     for (uint32_t i = 0; i < 4; i++) {
         if (got < 4) acc |= (uint64_t)(uint32_t)e4[i] << (8 * got);
-        got += (uint32_t)(e4[i] >> 56) & 7u;
+        got += HH_FSM_ET_NSYM(e4[i]);
     }
     if (got < need) {
         acc = 0;
@@ -530,12 +578,13 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
     if (at_end && s != 0) dst[o] = ts[s];
 }
 
-template <uint32_t SW, uint32_t K>
+template <uint32_t SW, uint32_t K, bool TAIL>
 __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
-                                                 uint8_t *__restrict__ out, uint64_t cap) {
+                                                 uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW;
-    const uint32_t ns = geo.ns, r = geo.r, tid = threadIdx.x, j = tid & 63u, wv = tid >> 6;
+    const uint32_t ns = geo.ns, r = geo.r, tid = threadIdx.x, j = tid & 63u;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // (uniform: scalar tile index)
     const uint32_t er_off = (ns << K) * 8u;
     uint32_t *s_b1 = (uint32_t *)(smem + er_off + (r ? (ns << r) * 8u : 0u));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
@@ -547,12 +596,11 @@ __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g,
     __syncthreads();
 
     const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * EW;
-    const uint64_t nfast = geo.bits / TB;         // tiles that end before the stream does
-    const uint64_t tlast = geo.ntiles - 1;        // (launched only when emit_from < ntiles)
     // next tile's words, record, correction and base, loaded one tile ahead
     // (the base words by lanes 0..2, read out with readlane where consumed)
     uint32_t pw[SW], prec = 0, pfx = 0, pmeta = 0;
     auto prefetch = [&](uint64_t tt) {
+        tt = uni64(tt);
         const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
         prec = wk.rec[tt * NR + j];
         pfx = wk.fx[tt * FX_W + (j & (FX_W - 1))];
@@ -561,9 +609,9 @@ __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g,
         pmeta = *(ln == 0 ? blk32 : ln == 1 ? blk32 + 1 : (const uint32_t *)&wk.lex[tt]);
         fs_load<SW>(pw, rs, j * SW);
     };
-    uint64_t t = geo.emit_from + (uint64_t)blockIdx.x * EW + wv;
-    if (t < geo.ntiles) prefetch(t);
-    for (; t < geo.ntiles; t += nwv) {
+    uint64_t t = t0 + (uint64_t)blockIdx.x * EW + wv;
+    if (t < t1) prefetch(t);
+    for (; t < t1; t += nwv) {
         uint32_t w[SW];
 #pragma unroll
         for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
@@ -571,7 +619,7 @@ __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g,
         const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)pmeta, 0);
         const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)pmeta, 1);
         const int32_t lx = __builtin_amdgcn_readlane((int)pmeta, 2);
-        prefetch(t + nwv < geo.ntiles ? t + nwv : tlast);
+        prefetch(t + nwv < t1 ? t + nwv : t);
         uint32_t ent = fsm_rec_ent(rc);
         int32_t cnt = (int32_t)fsm_rec_cnt(rc);
         if (fsm_fx_ok(fx)) {
@@ -589,8 +637,7 @@ __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g,
         const uint64_t R = t * TB + (uint64_t)j * S;
         uint32_t lim = S;
         bool at_end = R + S == geo.bits;
-        const bool tail = t >= nfast;
-        if (tail) {
+        if (TAIL) {
             lim = R >= geo.bits ? 0u : (geo.bits - R < S ? (uint32_t)(geo.bits - R) : S);
             at_end = R < geo.bits && R + S >= geo.bits;
         }
@@ -600,8 +647,7 @@ __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g,
             uint64_t e4[4];
             uint32_t lw = 0, lwd = 0;
             WAVE_SYNC();                              // the previous tile's copy-out has read the staging
-            if (!tail) emf_region<SW, K, false>(smem, er_off, r, s_b1, s_ts, w, ent, lim, at_end, oa, e4, &lw, &lwd);
-            else emf_region<SW, K, true>(smem, er_off, r, s_b1, s_ts, w, ent, lim, at_end, oa, e4, &lw, &lwd);
+            emf_region<SW, K, TAIL>(smem, er_off, r, s_b1, s_ts, w, ent, lim, at_end, oa, e4, &lw, &lwd);
             WAVE_SYNC();
             emf_edges<SW, K>(smem, s_b1, s_ts, w, ent, lim, at_end, c, oa, e4, lw, lwd);
             WAVE_SYNC();
@@ -627,21 +673,24 @@ __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g,
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
-typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork);
-typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t);
+typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint64_t);
+typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t);
 
 #define FSM_SW_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
-static kcnt_t kcnt_for(uint32_t sw) {
+static kcnt_t kcnt_for(uint32_t sw, bool tail) {
     switch (sw) {
-#define X(n) case n: return k_cnt<n>;
+#define X(n) case n: return tail ? k_cnt<n, true> : k_cnt<n, false>;
         FSM_SW_CASES(X)
 #undef X
     default: return nullptr;
     }
 }
-static kemf_t kemf_for(uint32_t sw, uint32_t K) {
+static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail) {
     switch (sw) {
-#define X(n) case n: return K == 6 ? k_emf<n, 6> : K == 4 ? k_emf<n, 4> : nullptr;
+#define X(n)                                                                            \
+    case n:                                                                             \
+        return K == 6 ? (tail ? k_emf<n, 6, true> : k_emf<n, 6, false>)                 \
+                      : K == 4 ? (tail ? k_emf<n, 4, true> : k_emf<n, 4, false>) : nullptr;
         FSM_SW_CASES(X)
 #undef X
     default: return nullptr;
@@ -688,8 +737,8 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G) {
 static int fsm_grids(FsmDev *fd) {
     if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns) return HH_OK;
     const uint32_t sw = fd->S / 32;
-    const kcnt_t kc = kcnt_for(sw);
-    const kemf_t ke = kemf_for(sw, fd->K);
+    const kcnt_t kc = kcnt_for(sw, false);
+    const kemf_t ke = kemf_for(sw, fd->K, false);
     if (!kc || !ke) return HH_ERR_UNSUPPORTED;
     int pc = 0, pe = 0, ncu = 0, dev = 0;
     FS_OK(hipGetDevice(&dev));
@@ -752,15 +801,25 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     wk.blk = (int64_t *)(w + o_blk);
     FsmTab tab = {fd->ct, fd->b1, fd->tsym, fd->et, fd->er};
     const uint32_t sw = fd->S / 32;
-    const kcnt_t kc = kcnt_for(sw);
-    const kemf_t ke = kemf_for(sw, fd->K);
     FS_OK(hipMemsetAsync(wk.flags, 0, 64, st));
     FS_OK(hipEventRecord(ev[0], st));
     {
-        const uint64_t nwg = (nt + CW - 1) / CW;
-        const uint32_t gc = (uint32_t)(nwg < fd->grid_c ? nwg : fd->grid_c);
-        hipLaunchKernelGGL(kc, dim3(gc), dim3(64 * CW), lds_cnt(fd), st, (const uint32_t *)d_data, geo, tab, wk);
-        FS_OK(hipGetLastError());
+        // tiles [0, nc) whose regions and next region end before the stream,
+        // then the last ones (TAIL)
+        const uint64_t S = fd->S;
+        const uint64_t nc = bits > TB + S ? std::min<uint64_t>((bits - S - 1) / TB, nt) : 0;
+        if (nc) {
+            const uint64_t nwg = (nc + CW - 1) / CW;
+            const uint32_t gc = (uint32_t)(nwg < fd->grid_c ? nwg : fd->grid_c);
+            hipLaunchKernelGGL(kcnt_for(sw, false), dim3(gc), dim3(64 * CW), lds_cnt(fd), st, (const uint32_t *)d_data,
+                               geo, tab, wk, (uint64_t)0, nc);
+            FS_OK(hipGetLastError());
+        }
+        if (nc < nt) {
+            hipLaunchKernelGGL(kcnt_for(sw, true), dim3((unsigned)((nt - nc + CW - 1) / CW)), dim3(64 * CW), lds_cnt(fd),
+                               st, (const uint32_t *)d_data, geo, tab, wk, nc, nt);
+            FS_OK(hipGetLastError());
+        }
     }
     FS_OK(hipEventRecord(ev[1], st));
     hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk);
@@ -769,11 +828,20 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     FS_OK(hipGetLastError());
     FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
-        const uint64_t ne = nt - emit_from, nwg = (ne + EW - 1) / EW;
-        const uint32_t ge = (uint32_t)(nwg < fd->grid_e ? nwg : fd->grid_e);
-        hipLaunchKernelGGL(ke, dim3(ge), dim3(64 * EW), lds_emf(fd), st, (const uint32_t *)d_data, geo, tab, wk,
-                           (uint8_t *)d_out, cap);
-        FS_OK(hipGetLastError());
+        // tiles that end before the stream, then the last one(s) (TAIL)
+        const uint64_t ne = std::max<uint64_t>(emit_from, std::min<uint64_t>(bits / TB, nt));
+        if (ne > emit_from) {
+            const uint64_t nwg = (ne - emit_from + EW - 1) / EW;
+            const uint32_t ge = (uint32_t)(nwg < fd->grid_e ? nwg : fd->grid_e);
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, false), dim3(ge), dim3(64 * EW), lds_emf(fd), st,
+                               (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne);
+            FS_OK(hipGetLastError());
+        }
+        if (ne < nt) {
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, true), dim3((unsigned)((nt - ne + EW - 1) / EW)), dim3(64 * EW),
+                               lds_emf(fd), st, (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt);
+            FS_OK(hipGetLastError());
+        }
     }
     FS_OK(hipEventRecord(ev[3], st));
     FS_OK(hipMemcpyAsync(h_flags, wk.flags, 64, hipMemcpyDeviceToHost, st));

@@ -67,7 +67,7 @@ HH_FD uint32_t hh_fsm_pick_head(const hh_tables *t) {
 }
 
 typedef struct {
-    const uint16_t *ct;      /* 8-bit steps: next | completed << 8 */
+    const uint16_t *ct;      /* 8-bit steps: next << 9 | completed */
     const uint32_t *b1;      /* 1-bit steps: next | completed << 8 | sym << 16 */
     const uint8_t *tsym;     /* tail-rule symbol of a state */
 } hh_fsm_view;
@@ -89,8 +89,8 @@ HH_FD uint32_t fsm_run(const hh_fsm_view *F, const uint32_t *w, uint64_t p, uint
     }
     while (p + 8 <= e) {
         const uint32_t v = F->ct[s * 256 + fsm_byte(w, p)];
-        s = v & 255u;
-        c += v >> 8;
+        s = HH_FSM_CT_NEXT(v);
+        c += HH_FSM_CT_CNT(v);
         p += 8;
     }
     while (p < e) {
@@ -134,7 +134,10 @@ HH_FD int fsm_walk2(const hh_fsm_view *F, const uint32_t *w, uint64_t R, uint64_
             va = F->ct[a * 256 + x];
             vb = F->ct[b * 256 + x];
             p += 8;
-            dd += (int32_t)(va >> 8) - (int32_t)(vb >> 8);
+            dd += (int32_t)HH_FSM_CT_CNT(va) - (int32_t)HH_FSM_CT_CNT(vb);
+            a = HH_FSM_CT_NEXT(va);
+            b = HH_FSM_CT_NEXT(vb);
+            continue;
         } else {
             const uint32_t x = fsm_bit(w, p);
             va = F->b1[a * 2 + x];

@@ -475,7 +475,7 @@ int hh_fsm_build(const void *tv, uint32_t S, hh_fsm_tables *F) {
         uint32_t sy, n;
         for (uint32_t v = 0; v < 256; v++) {
             const uint32_t to = fsm_walk(T, nd, v, 8, 0, &sy, &n);
-            F->ct[s * 256 + v] = (uint16_t)((uint32_t)st[to] | (n << 8));
+            F->ct[s * 256 + v] = (uint16_t)(((uint32_t)st[to] << 9) | n);
         }
         for (uint32_t bit = 0; bit < 2; bit++) {
             const uint32_t to = fsm_walk(T, nd, bit, 1, 1, &sy, &n);
@@ -484,13 +484,11 @@ int hh_fsm_build(const void *tv, uint32_t S, hh_fsm_tables *F) {
         const uint32_t K = F->K;
         for (uint32_t v = 0; v < (1u << K); v++) {
             const uint32_t to = fsm_walk(T, nd, v, K, 4, &sy, &n);
-            F->et[(s << K) | v] = (uint64_t)sy | ((uint64_t)((uint32_t)st[to] << (K + 3)) << 32) |
-                                  ((uint64_t)n << 56);
+            F->et[(s << K) | v] = HH_FSM_ET_MAKE(sy, (uint32_t)st[to] << (K + 3), n);
         }
         for (uint32_t v = 0; F->r && v < (1u << F->r); v++) {
             const uint32_t to = fsm_walk(T, nd, v, F->r, 4, &sy, &n);
-            F->er[(s << F->r) | v] = (uint64_t)sy | ((uint64_t)((uint32_t)st[to] << (K + 3)) << 32) |
-                                     ((uint64_t)n << 56);
+            F->er[(s << F->r) | v] = HH_FSM_ET_MAKE(sy, (uint32_t)st[to] << (K + 3), n);
         }
     }
 out:

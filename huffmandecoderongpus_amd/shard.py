@@ -115,6 +115,34 @@ def out_base(rows: list, rank: int) -> int:
     return int(sum(int(rows[r][4]) for r in range(rank)))
 
 
+def assemble(local, n: int, rows: list, dist, world: int):
+    """The global output from the ranks' segments: one all-gather of the
+    segments padded to the largest (RCCL: all_gather_into_tensor on the
+    GPU; gloo: host tensors), then rank r's first out_len bytes in rank
+    order.  `local` is this rank's segment buffer (n bytes valid).  Returns
+    (the gathered padded buffer, the padded length)."""
+    import torch
+    mx = max(int(r[4]) for r in rows)
+    gloo = dist.get_backend() == "gloo"
+    dev = torch.device("cpu") if gloo else local.device
+    pad = torch.zeros(max(mx, 1), dtype=torch.uint8, device=dev)
+    pad[:n] = local[:n].to(dev)
+    if gloo:
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad)
+        big = torch.cat(parts)
+    else:
+        big = torch.empty(pad.numel() * world, dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(big, pad)
+    return big, pad.numel()
+
+
+def concat(big, mx: int, rows: list):
+    """The stream's symbols from assemble()'s buffer."""
+    import torch
+    return torch.cat([big[r * mx:r * mx + int(rows[r][4])] for r in range(len(rows))])
+
+
 class ShardJob:
     """One rank's shard of the synthetic workload on its GPU: the global
     stream is `world` x target_bytes of tiled kjv.txt (cut at a symbol), this
@@ -158,16 +186,13 @@ class ShardJob:
 
     def _decode(self, in_state: int, prologue: int) -> dict:
         s = self.seg
-        if s.t1 == s.t0:
-            # no owned tile (fewer tiles than ranks): nothing to decode, and
-            # the chain leaves this rank in the state it entered
-            return {"out_len": 0, "leave_state": in_state, "const_seen": False,
-                    "entry_state": in_state, "entry_exact": prologue == 0, "in_state": in_state}
         skip = (s.prologue - prologue) * s.tile_bits          # bits, multiple of 32
+        # (no owned tile, fewer tiles than ranks: ntiles 0, and the range
+        # decode leaves the chain in the state it entered)
+        nt = s.ntiles - (s.prologue - prologue) if s.t1 > s.t0 else 0
         r = self.dec.decode_range_ptr(self.syn.data.data_ptr() + skip // 8,
-                                      s.bits_avail - skip, s.ntiles - (s.prologue - prologue),
-                                      in_state, self.out.data_ptr(), self.cap,
-                                      self.stream.cuda_stream, prologue=prologue)
+                                      s.bits_avail - skip, nt, in_state, self.out.data_ptr(),
+                                      self.cap, self.stream.cuda_stream, prologue=prologue)
         r["in_state"] = r["entry_state"]
         return r
 
@@ -202,33 +227,38 @@ class ShardJob:
         return True
 
     def gather_report(self) -> dict:
-        """All-gather of the decoded segments (padded to the largest), timed
-        outside the decode steps: the assembly cost, reported separately."""
+        """All-gather of the decoded segments (assemble()), timed outside
+        the decode steps: the assembly cost, reported separately.  Rank 0
+        then checks every rank's part of the assembled stream against the
+        tiled text from that rank's base."""
         import torch
         n = self.decoded_bytes
-        mx = max(int(r[4]) for r in self.rows)
-        pad = torch.zeros(mx, dtype=torch.uint8, device=self.dev)
-        pad[:n] = self.out[:n]
-        big = torch.empty(mx * self.world, dtype=torch.uint8, device=self.dev)
         self._dist.barrier()
         torch.cuda.synchronize(self.dev)
         t0 = time.perf_counter()
-        self._dist.all_gather_into_tensor(big, pad)
-        torch.cuda.synchronize(self.dev)
+        big, mx = assemble(self.out, n, self.rows, self._dist, self.world)
+        if big.is_cuda:
+            torch.cuda.synchronize(self.dev)
         t = time.perf_counter() - t0
-        tt = torch.tensor([t], dtype=torch.float64, device=self.dev)
+        tt = torch.tensor([t], dtype=torch.float64)
+        if self._dist.get_backend() != "gloo":
+            tt = tt.to(self.dev)
         self._dist.all_reduce(tt, op=self._dist.ReduceOp.MAX)
         t = float(tt.item())
         ok = True
-        if self.rank == 0:      # spot-check the assembled stream at every seam
+        if self.rank == 0:
             L = self.text.numel()
+            text = self.text.to(big.device)
+            step = 1 << 28
             for r in range(self.world):
-                b = out_base(self.rows, r)
-                k = min(4096, int(self.rows[r][4]))
-                idx = (torch.arange(k, device=self.dev, dtype=torch.int64) + b) % L
-                ok = ok and torch.equal(big[r * mx:r * mx + k], self.text[idx])
-        del big, pad
+                b, k = out_base(self.rows, r), int(self.rows[r][4])
+                for o in range(0, k, step):
+                    m = min(step, k - o)
+                    idx = (torch.arange(m, device=big.device, dtype=torch.int64) + (b + o)) % L
+                    ok = ok and torch.equal(big[r * mx + o:r * mx + o + m], text[idx])
+            ok = ok and out_base(self.rows, self.world) == self.total_syms
+        del big
         torch.cuda.empty_cache()
         return {"allgather": {"ms": round(t * 1e3, 3), "bytes_per_rank": mx * self.world,
-                              "GBps_in_per_rank": round(mx * (self.world - 1) / t / 1e9, 1),
+                              "GBps_in_per_rank": round(mx * (self.world - 1) / max(t, 1e-9) / 1e9, 1),
                               "seams_ok": bool(ok)}}

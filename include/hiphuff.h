@@ -185,9 +185,11 @@ int hh_decode_device(hh_decoder *dec, const void *d_data, uint64_t bits,
 /* ---------------------------------------------------------------------- */
 /* Segments (multi-GPU shards).  The stream is cut into tiles of           */
 /* hh_decoder_tile_bits() bits; a segment is a run of whole tiles.  The    */
-/* chain enters a segment in a STATE (region, offset, count correction) */
-/* that is the state leaving the previous segment; the stream starts in   */
-/* state 0.  A segment's output is the symbols from its entry point up to */
+/* chain enters a segment in a STATE that is the state leaving the       */
+/* previous segment; the stream starts in state 0.  States are opaque     */
+/* 32-bit values of the decoder's (a node of the code tree on the state-  */
+/* machine path): pass a predecessor's leave_state on unchanged, for the  */
+/* same tree.  A segment's output is the symbols from its entry point up to */
 /* its successor's, i.e. the segments' outputs concatenate to the stream's */
 /* (the reference has no multi-device path).              */
 /* ---------------------------------------------------------------------- */
@@ -198,7 +200,10 @@ typedef struct {
                                 tiles plus at least one tile after them (the
                                 next segment's first regions), or up to the
                                 end of the stream for the last segment     */
-    uint64_t ntiles;         /* tiles to decode; 0 = all of bits_avail      */
+    uint64_t ntiles;         /* tiles to decode (prologue included; at most */
+                             /* the tiles of bits_avail).  0 decodes none:  */
+                             /* out_len 0, leave_state = entry_state =      */
+                             /* in_state, entry_exact = (prologue == 0)     */
     uint64_t prologue;       /* the first `prologue` tiles are the end of   */
                              /* the PREVIOUS segment: decoded only to find  */
                              /* the state entering tile `prologue`, where   */

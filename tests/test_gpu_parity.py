@@ -250,6 +250,35 @@ def test_synthetic_full_size(hh, files_dir, src, mib):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("chunk_kb,mib", [(None, 1024), (4096, 64), (2, 1)])
+def test_evaluate_scope_pipeline(hh, files_dir, chunk_kb, mib, monkeypatch):
+    """hh_decode_host (the reference's evaluate() scope) uploads the payload
+    in chunks, decodes each as a segment entered in the state the previous
+    one left and downloads its symbols while later chunks are in flight: the
+    bytes must equal the tiled text however many chunks the stream is cut
+    into (the default 128 MiB chunks on the 1 GiB stream; 4 MiB chunks; 2 KiB
+    chunks, one tile each, on 1 MiB)."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    if chunk_kb:
+        monkeypatch.setenv("HH_PIPE_CHUNK_KB", str(chunk_kb))
+    hf, text = synth.load_source(files_dir, "kjv.txt")
+    syn = synth.tiled_stream(hf, text, mib << 20)
+    host = syn.data[: syn.compressed_bytes].cpu().numpy()
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(syn.tree)
+        buf = np.full(syn.decoded_bytes + 64, 0xAB, np.uint8)
+        for _ in range(2):
+            out = dec.decode_host(host, syn.bits, syn.decoded_bytes + 16, out=buf)
+            assert len(out) == syn.decoded_bytes
+            assert synth.verify_tiled(torch.from_numpy(out).cuda(), syn)
+            assert (buf[syn.decoded_bytes + 16:] == 0xAB).all()
+            assert dec.stats()["state_machine"] == 1
+    finally:
+        dec.close()
+
+
 @pytest.mark.parametrize("env", [{"HH_FRONT_WALK": "2"}, {"HH_FRONT_WALK": "16"},
                                  {"HH_FRONT_WALK": "8192"}, {"HH_EMIT_XPT": "0"},
                                  {"HH_EMIT_XPT": "1"}, {"HH_EMIT_NW": "8"}])
@@ -346,16 +375,19 @@ def test_hufx_over_2gib_save_reload_decode(hh, files_dir, tmp_path):
         torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("world,probe", [(3, 2), (5, 1), (4, 0)])
-def test_segments_concatenate(hh, files_dir, world, probe):
+@pytest.mark.parametrize("name,world,probe", [("kjv.txt", 3, 2), ("kjv.txt", 5, 1), ("kjv.txt", 4, 0),
+                                               ("hello", 4, 2), ("paper1", 40, 2)])
+def test_segments_concatenate(hh, files_dir, name, world, probe):
     """hh_decode_device_range on one GPU, shards planned as bench.py --gpus N
     plans them, each with `probe` predecessor tiles as a prologue; every
     "rank" is a thread running shard.settle over an in-process gather (one
     decoder, calls serialised).  probe 0: entries are guesses that the
-    exchange must catch.  The outputs must concatenate to the oracle's."""
+    exchange must catch.  hello (1 tile) and paper1 (< 40 tiles): more ranks
+    than tiles, the empty shards pass ntiles 0.  The outputs must
+    concatenate to the oracle's."""
     import torch
     from huffmandecoderongpus_amd import shard
-    path = os.path.join(files_dir, "kjv.txt.huff")
+    path = os.path.join(files_dir, name + ".huff")
     hf = hh.HuffFile.load(path)
     ref = O.OracleHuff.load(path).chain_decode()
     dec = hh.Decoder(0)
@@ -369,9 +401,12 @@ def test_segments_concatenate(hh, files_dir, world, probe):
         final, redone = _settle_segments(dec, pay, segs, outs)
         got = torch.cat([outs[r][:final[r]["out_len"]] for r in range(world)]).cpu().numpy()
         assert len(got) == len(ref) and np.array_equal(got, ref)
+        ntiles = (hf.bits + tb - 1) // tb
         if probe:
-            assert sum(redone) == 0
-        else:
+            # (a rank without a tile of its own takes its predecessor's leave
+            # state in one exchange round: only those are redone)
+            assert sum(n for n, s in zip(redone, segs) if s.t1 > s.t0) == 0
+        elif ntiles >= world:
             assert sum(redone) >= 1
     finally:
         dec.close()
@@ -396,12 +431,11 @@ def _settle_segments(dec, pay, segs, outs):
     def run(r, in_state, prologue):
         s = segs[r]
         skip = s.prologue - prologue
-        if s.t1 == s.t0:
-            return {"out_len": 0, "leave_state": in_state, "const_seen": False,
-                    "entry_state": in_state, "entry_exact": prologue == 0, "in_state": in_state}
         with lock:
+            # (a shard with no tile of its own: ntiles 0 through the C ABI)
             res = dec.decode_range_ptr(pay.data_ptr() + (s.buf_bit + skip * tb) // 8,
-                                       s.bits_avail - skip * tb, s.ntiles - skip, in_state,
+                                       s.bits_avail - skip * tb,
+                                       s.ntiles - skip if s.t1 > s.t0 else 0, in_state,
                                        outs[r].data_ptr(), outs[r].numel(), 0,
                                        prologue=prologue)
             torch.cuda.synchronize()
@@ -492,6 +526,8 @@ def _shard_rank(rank, world, port, mib, q):
             job.decode_step()
             torch.cuda.synchronize()
             ok = ok and job.verify()
+        rep = job.gather_report()            # the assembled stream (gloo: host tensors)
+        ok = ok and rep["allgather"]["seams_ok"]
         q.put((rank, ok, job.decoded_bytes, job.seg.prologue))
         dist.barrier()
         dist.destroy_process_group()
@@ -504,8 +540,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_shard_job_two_ranks_one_gpu():
     """bench.py's multi-GPU path (ShardJob: shard plan, prologue entry,
-    settle exchange, per-rank verification against the tiled text) with two
-    processes sharing GPU 0 over gloo (RCCL needs distinct GPUs)."""
+    settle exchange, per-rank verification against the tiled text, the
+    all-gather assembly checked on rank 0) with two processes sharing GPU 0
+    over gloo (RCCL needs distinct GPUs)."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()

@@ -21,6 +21,8 @@ E.hh_fsm_emu_decode.restype = C.c_int64
 E.hh_fsm_emu_decode.argtypes = [C.c_void_p] * 3 + [C.c_int32, C.c_void_p, C.c_uint64, C.c_uint32, C.c_int32,
                                                    C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64,
                                                    C.c_void_p, C.c_void_p, C.c_void_p]
+E.hh_fsm_emu_arrays.restype = C.c_int64
+E.hh_fsm_emu_arrays.argtypes = [C.c_void_p] * 4
 iz = np.ascontiguousarray(hf.izero, np.int32)
 io = np.ascontiguousarray(hf.ione, np.int32)
 sy = np.ascontiguousarray(hf.sym, np.uint8)
