@@ -459,29 +459,32 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
 }
 
 // Region j entered in state s, its symbols to the staging from LDS byte
-// address oa on: K-bit steps, each step's symbols shifted into a 64-bit
-// accumulator whose low dword is stored to its aligned LDS dword every step
-// (a dword is stored again until it is full: no branch), then the r-bit
-// step; TAIL: steps while whole, the rest bit by bit, and the tail rule.
-// The unused bytes of every stored dword are zero: a dword shared with the
-// neighbouring runs is repaired by OR afterwards (emf_edges).  e4 receives
-// the first four steps' entries; *lastw / *lastwd the run's last dword.
+// address oa on: K-bit steps, each step's symbols shifted into the current
+// dword, which is stored to its aligned LDS address every step (a dword is
+// stored again until it is full: no branch), then the r-bit step (r = S mod
+// K); TAIL: steps while whole, the rest bit by bit, and the tail rule.  The
+// unused bytes of every stored dword are zero: a dword shared with the
+// neighbouring runs is repaired by OR afterwards (emf_edges).  *first: the
+// run's bytes in its first dword (valid when *first_ok), *lastw / *lastwd:
+// the run's last dword.
+#define EMF_KE 8          // steps within which the first dword is captured
 template <uint32_t SW, uint32_t K, bool TAIL>
-__device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, uint32_t r, const uint32_t *b1,
-                                           const uint8_t *ts, const uint32_t *w, uint32_t s, uint32_t lim,
-                                           bool at_end, uint32_t oa, uint64_t *e4, uint32_t *lastw,
-                                           uint32_t *lastwd) {
-    constexpr uint32_t S = 32 * SW;
+__device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const uint32_t *b1, const uint8_t *ts,
+                                           const uint32_t *w, uint32_t s, uint32_t lim, bool at_end, uint32_t oa,
+                                           uint32_t *first, bool *first_ok, uint32_t *lastw, uint32_t *lastwd) {
+    constexpr uint32_t S = 32 * SW, r = S % K;
     uint32_t row = s << (K + 3);
-    uint32_t wd = oa & ~3u, sh = (oa & 3u) * 8u;
+    const uint32_t wd0 = oa & ~3u;
+    uint32_t wd = wd0, sh = (oa & 3u) * 8u;
     uint32_t a = 0;                                 // the current dword's bytes so far
-    auto put = [&](uint64_t e) {
+    auto put = [&](uint64_t e) -> uint32_t {
         const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
         const uint32_t u = sh + ((hi >> 8) & 255u);   // 8 x the symbols: one SDWA add
+        uint32_t an;
         if (K == 6) {
             // <= 3 symbol bytes: what does not fit the current dword spills
             // into the next (nothing spills when sh = 0)
-            const uint32_t an = (lo << sh) | a;
+            an = (lo << sh) | a;
             const uint32_t sp = __builtin_amdgcn_alignbit(0u, lo, (0u - sh) & 31u);
             *(uint32_t *)(lds + wd) = an;
             const bool full = u >= 32;
@@ -490,24 +493,27 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, uint32
         } else {
             // <= 4 bytes (1-bit codes): a 64-bit shift
             const uint64_t acc = (uint64_t)a | ((uint64_t)lo << sh);
-            *(uint32_t *)(lds + wd) = (uint32_t)acc;
+            an = (uint32_t)acc;
+            *(uint32_t *)(lds + wd) = an;
             const bool full = u >= 32;
-            a = full ? (uint32_t)(acc >> 32) : (uint32_t)acc;
+            a = full ? (uint32_t)(acc >> 32) : an;
             wd += full ? 4u : 0u;
         }
         sh = u & 31u;
+        return an;
     };
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) e4[i] = 0;
+    uint32_t fw = 0, wdk = wd0;
 #pragma unroll
     for (uint32_t k = 0; k < S / K; k++) {
         const uint32_t q = k * K;
         if (!TAIL || q + K <= lim) {
             const uint64_t e = *(const uint64_t *)(lds + row + win8<SW, K>(w, q));
-            put(e);
+            const uint32_t at = wd;
+            const uint32_t v = put(e);
+            if (k < EMF_KE) fw = at == wd0 ? v : fw;       // the last value stored to the first dword
             row = (uint32_t)(e >> 48);
-            if (k < 4) e4[k] = e;
         }
+        if (k + 1 == EMF_KE) wdk = wd;
     }
     if (!TAIL) {
         if (r) {
@@ -526,40 +532,36 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, uint32
     }
     if (at_end && (row >> (K + 3)) != 0) put(HH_FSM_ET_MAKE(ts[row >> (K + 3)], 0u, 1u));   // the tail rule
     *(uint32_t *)(lds + wd) = a;                     // the bytes of the last step's overflow
+    // the first dword: complete in fw once the run left it within EMF_KE
+    // steps; the final dword when the run never left it
+    *first = wd == wd0 ? a : fw;
+    *first_ok = wd == wd0 || wdk != wd0 || (S / K < EMF_KE);
     *lastw = a;
     *lastwd = wd;
 }
 
 // After every lane's stores: the dwords a run shares with its neighbours hold
 // one run's bytes (and zeros); each run ORs its own bytes back into its first
-// and last dword.  The first dword's bytes come from the first four steps'
-// entries (or, when those hold too few symbols, a bit-serial re-run).
+// and last dword.  The first dword's bytes were captured by emf_region (a
+// bit-serial re-run when the run left its first dword late).
 template <uint32_t SW, uint32_t K>
 __device__ __forceinline__ void emf_edges(uint8_t *lds, const uint32_t *b1, const uint8_t *ts, const uint32_t *w,
                                           uint32_t s, uint32_t lim, bool at_end, uint32_t cnt, uint32_t oa,
-                                          const uint64_t *e4, uint32_t lastw, uint32_t lastwd) {
+                                          uint32_t first, bool first_ok, uint32_t lastw, uint32_t lastwd) {
     if (!cnt) return;
     const uint32_t b0 = oa & 3u;
-    const uint32_t need = 4u - b0 < cnt ? 4u - b0 : cnt;   // the run's bytes in its first dword
-    uint64_t acc = 0;
-    uint32_t got = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 4; i++) {
-        if (got < 4) acc |= (uint64_t)(uint32_t)e4[i] << (8 * got);
-        got += HH_FSM_ET_NSYM(e4[i]);
-    }
-    if (got < need) {
-        acc = 0;
-        got = 0;
-        uint32_t st = s;
+    uint32_t firstw = first;
+    if (!first_ok) {
+        const uint32_t need = 4u - b0 < cnt ? 4u - b0 : cnt;   // the run's bytes in its first dword
+        uint32_t acc = 0, got = 0, st = s;
         for (uint32_t q = 0; q < lim && got < need; q++) {
             const uint32_t v = b1[st * 2 + rbit_dyn<SW>(w, q)];
             st = v & 255u;
-            if ((v >> 8) & 255u) acc |= (uint64_t)((v >> 16) & 255u) << (8 * got++);
+            if ((v >> 8) & 255u) acc |= ((v >> 16) & 255u) << (8 * got++);
         }
-        if (got < need && at_end && st != 0) acc |= (uint64_t)ts[st] << (8 * got++);
+        if (got < need && at_end && st != 0) acc |= (uint32_t)ts[st] << (8 * got++);
+        firstw = acc << (8 * b0);
     }
-    const uint32_t firstw = ((uint32_t)acc & (need == 4 ? 0xffffffffu : ((1u << (8 * need)) - 1u))) << (8 * b0);
     atomicOr((uint32_t *)(lds + (oa & ~3u)), firstw);
     if (lastwd != (oa & ~3u) && lastw) atomicOr((uint32_t *)(lds + lastwd), lastw);
 }
@@ -644,26 +646,26 @@ __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g,
         const uint32_t a0 = (uint32_t)(P0 & 15u);
         if (a0 + Tout + 8 <= OBW) {
             const uint32_t oa = stage + a0 + L;
-            uint64_t e4[4];
-            uint32_t lw = 0, lwd = 0;
+            uint32_t fw = 0, lw = 0, lwd = 0;
+            bool fok = true;
             WAVE_SYNC();                              // the previous tile's copy-out has read the staging
-            emf_region<SW, K, TAIL>(smem, er_off, r, s_b1, s_ts, w, ent, lim, at_end, oa, e4, &lw, &lwd);
+            emf_region<SW, K, TAIL>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, &fw, &fok, &lw, &lwd);
             WAVE_SYNC();
-            emf_edges<SW, K>(smem, s_b1, s_ts, w, ent, lim, at_end, c, oa, e4, lw, lwd);
+            emf_edges<SW, K>(smem, s_b1, s_ts, w, ent, lim, at_end, c, oa, fw, fok, lw, lwd);
             WAVE_SYNC();
-            // copy-out: whole 16-B blocks, the two partial ones byte by byte
+            // copy-out: whole 16-B blocks; the bytes of the partial first and
+            // last blocks one per lane (lanes 0..15, 16..31)
             uint8_t *gb = out + (P0 - a0);
             const uint8_t *sb = smem + stage;
-            const uint32_t nq = (a0 + Tout + 15u) / 16u;
+            const uint32_t end = a0 + Tout, nq = (end + 15u) / 16u;
             for (uint32_t i = j; i < nq; i += 64) {
                 const uint32_t lo = 16 * i;
-                if (lo >= a0 && lo + 16 <= a0 + Tout) {
+                if (lo >= a0 && lo + 16 <= end)
                     __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
-                } else {
-                    const uint32_t e = lo + 16 < a0 + Tout ? lo + 16 : a0 + Tout;
-                    for (uint32_t q = lo > a0 ? lo : a0; q < e; q++) gb[q] = sb[q];
-                }
             }
+            const bool part0 = a0 != 0 || end < 16, partl = (end & 15u) != 0 && end > 16;
+            const uint32_t q = j < 16 ? j : (end & ~15u) + (j - 16);
+            if (j < 32 && (j < 16 ? part0 : partl) && q >= a0 && q < end) gb[q] = sb[q];
         } else {
             emf_direct<SW>(s_b1, s_ts, w, ent, lim, at_end, out + P0 + L);
         }
