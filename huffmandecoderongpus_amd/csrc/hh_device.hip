@@ -1572,7 +1572,11 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     if (d->G > HH_GMAX || d->G + 32 > d->S) d->G = 0;
     // the state machine (trees of at most HH_FSM_MAXS internal nodes)
     fsm_free(&d->fsm);
-    if (d->S && hh_fsm_build(d->ht, d->S, d->ft) == HH_OK) {
+    // emission steps of 7 bits when the tables leave the staging room
+    // (fsm_k_fits), else 6 (HH_FSM_K: experiments)
+    uint32_t Kf = getenv("HH_FSM_K") ? (uint32_t)atoi(getenv("HH_FSM_K")) : 0u;
+    if (!Kf && d->S && hh_fsm_build(d->ht, d->S, 7, d->ft) == HH_OK && fsm_k_fits(d->ft)) Kf = 7;
+    if (d->S && hh_fsm_build(d->ht, d->S, Kf ? Kf : 6, d->ft) == HH_OK) {
         uint32_t Gf = hh_fsm_pick_head(d->ht);
         if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) & ~7u;   // experiments
         if (Gf > d->S) Gf = 0;

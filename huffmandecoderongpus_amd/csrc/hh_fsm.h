@@ -31,14 +31,11 @@
  *                     stream (its tail rule, decodeallbits.cl:20-31)
  *   et[s << K | v]    u64: K-bit steps (emission), v = the next K bits
  *       bits  0..31   the symbols completed (first in bits 0..7, unused
- *                     bytes 0): K = 6 for codes of >= 2 bits (<= 3
- *                     symbols, bits 24..31 then 0), K = 4 when a code has
- *                     1 bit (<= 4)
- *       bits 32..36   (32 - 8 x the number of symbols) mod 32: the rotation
- *                     that moves the K = 6 kernel's output position (a
- *                     one-hot multiplier) on
- *       bits 40..47   8 x the number of symbols
- *       bits 48..63   the next state's row in et, in bytes: next << (K + 3)
+ *                     bytes 0): K = 6 or 7 for codes of >= 2 bits, K = 4
+ *                     when a code has 1 bit; a step from inside a code
+ *                     completes up to 3 (K = 6) or 4 (K = 7, 4) symbols
+ *       bits 32..39   8 x the number of symbols (the output shift)
+ *       bits 47..63   the next state's row in et, in bytes: next << (K + 3)
  *   er[s << r | v]    u64: the r-bit step that ends a region of S bits when K
  *                     does not divide S (r = S mod K, 0: none); same layout,
  *                     rows in et units
@@ -58,16 +55,15 @@ typedef struct {
     uint16_t ct[HH_FSM_MAXS * 256];
     uint32_t b1[HH_FSM_MAXS * 2];
     uint8_t tsym[HH_FSM_MAXS + 1];
-    uint64_t et[HH_FSM_MAXS * 64];
-    uint64_t er[HH_FSM_MAXS * 32];
+    uint64_t et[HH_FSM_MAXS * 128];
+    uint64_t er[HH_FSM_MAXS * 64];
 } hh_fsm_tables;
 
 #define HH_FSM_ET_SYMS(e) ((uint32_t)(e))
-#define HH_FSM_ET_ROW(e) ((uint32_t)((e) >> 48))
-#define HH_FSM_ET_NSYM(e) ((uint32_t)((e) >> 43) & 31u)
-#define HH_FSM_ET_MAKE(syms, row, n)                                                    \
-    ((uint64_t)(uint32_t)(syms) | (uint64_t)((32u - 8u * (uint32_t)(n)) & 31u) << 32 | \
-     (uint64_t)(8u * (uint32_t)(n)) << 40 | (uint64_t)(uint32_t)(row) << 48)
+#define HH_FSM_ET_ROW(e) ((uint32_t)((e) >> 47))
+#define HH_FSM_ET_NSYM(e) ((uint32_t)((e) >> 35) & 31u)
+#define HH_FSM_ET_MAKE(syms, row, n) \
+    ((uint64_t)(uint32_t)(syms) | (uint64_t)(8u * (uint32_t)(n)) << 32 | (uint64_t)(uint32_t)(row) << 47)
 #define HH_FSM_CT_NEXT(v) ((uint32_t)(v) >> 9)
 #define HH_FSM_CT_CNT(v) ((uint32_t)(v) & 15u)
 
@@ -75,9 +71,10 @@ typedef struct {
 extern "C" {
 #endif
 /* Builds the state machine of the compact tree in T (hh_tables_build) for
- * regions of S bits.  HH_ERR_UNSUPPORTED when the tree has more than
- * HH_FSM_MAXS internal nodes. */
-int hh_fsm_build(const void *T /* const hh_tables* */, uint32_t S, hh_fsm_tables *F);
+ * regions of S bits, emission steps of K bits (6 or 7; 0: 6; a code of 1 bit
+ * takes K = 4 whatever is asked).  HH_ERR_UNSUPPORTED when the tree has more
+ * than HH_FSM_MAXS internal nodes. */
+int hh_fsm_build(const void *T /* const hh_tables* */, uint32_t S, uint32_t K, hh_fsm_tables *F);
 #ifdef __cplusplus
 }
 #endif

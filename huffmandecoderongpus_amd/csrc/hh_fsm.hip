@@ -45,8 +45,17 @@
 
 #define NR 64                 // regions per tile (a wave)
 #define CW 8                  // k_cnt: waves per workgroup
-#define EW 16                 // k_emf: waves per workgroup
-#define OBW 6144              // k_emf: output staging per wave (bytes); a kjv tile's output is ~3.7 KB
+// k_emf: waves per workgroup and output staging per wave (bytes) -- 7-bit
+// steps leave less room beside their tables (a kjv tile's output is ~1.8 KB
+// on average)
+#ifndef HH_EMF7_WAVES
+#define HH_EMF7_WAVES 12
+#endif
+#ifndef HH_EMF7_OBW
+#define HH_EMF7_OBW 5120
+#endif
+__host__ __device__ constexpr uint32_t emf_waves(uint32_t K) { return K == 7 ? HH_EMF7_WAVES : 16u; }
+__host__ __device__ constexpr uint32_t emf_obw(uint32_t K) { return K == 7 ? HH_EMF7_OBW : 6144u; }
 #define SCAN_TB 1024          // tiles per k_fscan1 block
 #define FX_W 8                // corrections per tile (HH_FSM_KM)
 static_assert(FX_W == HH_FSM_KM, "corrections per tile");
@@ -347,8 +356,11 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     }
 }
 
+#ifndef HH_CNT_WAVES
+#define HH_CNT_WAVES 4        // k_cnt: waves per SIMD the register budget is cut for
+#endif
 template <uint32_t SW, bool TAIL>
-__global__ __launch_bounds__(64 * CW) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+__global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint64_t t0, uint64_t t1) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW;
@@ -363,22 +375,19 @@ __global__ __launch_bounds__(64 * CW) void k_cnt(const uint32_t *__restrict__ g,
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts};
     const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * CW;
     uint64_t t = t0 + (uint64_t)blockIdx.x * CW + wv;
-    // the next tile's words are loaded one tile ahead
-    uint32_t pw[SW], pn[SW];
+    // the next tile's region words are loaded one tile ahead; region j+1's
+    // (used only by walks, well after the count) at the tile's start
+    uint32_t pw[SW];
     auto prefetch = [&](uint64_t tt) {
         tt = uni64(tt);
-        const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
-        fs_load<SW>(pw, rs, j * SW);
-        fs_load<SW>(pn, rs, (j + 1) * SW);
+        fs_load<SW>(pw, fs_rsrc(g, tt * TB / 32, geo.nwords), j * SW);
     };
     if (t < t1) prefetch(t);
     for (; t < t1; t += nwv) {
         uint32_t w[SW], nx[SW];
 #pragma unroll
-        for (uint32_t k = 0; k < SW; k++) {
-            w[k] = pw[k];
-            nx[k] = pn[k];
-        }
+        for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
+        fs_load<SW>(nx, fs_rsrc(g, uni64(t) * TB / 32, geo.nwords), (j + 1) * SW);
         prefetch(t + nwv < t1 ? t + nwv : t);
         cnt_tile<SW, TAIL>(smem, F, g, geo, wk, t, w, nx);
     }
@@ -479,26 +488,17 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
     uint32_t a = 0;                                 // the current dword's bytes so far
     auto put = [&](uint64_t e) -> uint32_t {
         const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
-        const uint32_t u = sh + ((hi >> 8) & 255u);   // 8 x the symbols: one SDWA add
-        uint32_t an;
-        if (K == 6) {
-            // <= 3 symbol bytes: what does not fit the current dword spills
-            // into the next (nothing spills when sh = 0)
-            an = (lo << sh) | a;
-            const uint32_t sp = __builtin_amdgcn_alignbit(0u, lo, (0u - sh) & 31u);
-            *(uint32_t *)(lds + wd) = an;
-            const bool full = u >= 32;
-            a = full ? sp : an;
-            wd += full ? 4u : 0u;
-        } else {
-            // <= 4 bytes (1-bit codes): a 64-bit shift
-            const uint64_t acc = (uint64_t)a | ((uint64_t)lo << sh);
-            an = (uint32_t)acc;
-            *(uint32_t *)(lds + wd) = an;
-            const bool full = u >= 32;
-            a = full ? (uint32_t)(acc >> 32) : an;
-            wd += full ? 4u : 0u;
-        }
+        const uint32_t u = sh + (hi & 255u);          // 8 x the symbols: one SDWA add
+        // the bytes that do not fit the current dword spill into the next;
+        // K = 6 steps carry at most 3 symbols, so nothing spills at sh = 0,
+        // K = 7 and K = 4 steps up to 4 (7 bits from inside a code: 1 + 3 x 2)
+        const uint32_t an = (lo << sh) | a;
+        uint32_t sp = __builtin_amdgcn_alignbit(0u, lo, (0u - sh) & 31u);
+        if (K != 6) sp = sh ? sp : 0u;
+        *(uint32_t *)(lds + wd) = an;
+        const bool full = u >= 32;
+        a = full ? sp : an;
+        wd += full ? 4u : 0u;
         sh = u & 31u;
         return an;
     };
@@ -511,7 +511,7 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
             const uint32_t at = wd;
             const uint32_t v = put(e);
             if (k < EMF_KE) fw = at == wd0 ? v : fw;       // the last value stored to the first dword
-            row = (uint32_t)(e >> 48);
+            row = HH_FSM_ET_ROW(e);
         }
         if (k + 1 == EMF_KE) wdk = wd;
     }
@@ -519,7 +519,7 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
         if (r) {
             const uint64_t e = *(const uint64_t *)(lds + er_off + (row >> (K - r)) + (rbits<SW>(w, S - r, r) << 3));
             put(e);
-            row = (uint32_t)(e >> 48);
+            row = HH_FSM_ET_ROW(e);
         }
     } else {
         uint32_t st = row >> (K + 3);
@@ -581,7 +581,7 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
 }
 
 template <uint32_t SW, uint32_t K, bool TAIL>
-__global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+__global__ __launch_bounds__(64 * emf_waves(K)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1) {
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW;
@@ -590,6 +590,7 @@ __global__ __launch_bounds__(64 * EW) void k_emf(const uint32_t *__restrict__ g,
     const uint32_t er_off = (ns << K) * 8u;
     uint32_t *s_b1 = (uint32_t *)(smem + er_off + (r ? (ns << r) * 8u : 0u));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
+    constexpr uint32_t EW = emf_waves(K), OBW = emf_obw(K);
     const uint32_t stage = emf_tab_bytes(ns, K, r) + wv * OBW;           // the wave's staging (LDS byte address)
     for (uint32_t i = tid; i < (ns << K); i += blockDim.x) ((uint64_t *)smem)[i] = tab.et[i];
     for (uint32_t i = tid; r && i < (ns << r); i += blockDim.x) ((uint64_t *)(smem + er_off))[i] = tab.er[i];
@@ -691,8 +692,9 @@ static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail) {
     switch (sw) {
 #define X(n)                                                                            \
     case n:                                                                             \
-        return K == 6 ? (tail ? k_emf<n, 6, true> : k_emf<n, 6, false>)                 \
-                      : K == 4 ? (tail ? k_emf<n, 4, true> : k_emf<n, 4, false>) : nullptr;
+        return K == 7   ? (tail ? k_emf<n, 7, true> : k_emf<n, 7, false>)               \
+               : K == 6 ? (tail ? k_emf<n, 6, true> : k_emf<n, 6, false>)               \
+               : K == 4 ? (tail ? k_emf<n, 4, true> : k_emf<n, 4, false>) : nullptr;
         FSM_SW_CASES(X)
 #undef X
     default: return nullptr;
@@ -700,7 +702,14 @@ static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail) {
 }
 
 static size_t lds_cnt(const FsmDev *fd) { return cnt_tab_bytes(fd->ns); }
-static size_t lds_emf(const FsmDev *fd) { return emf_tab_bytes(fd->ns, fd->K, fd->r) + (size_t)EW * OBW; }
+static size_t lds_emf(const FsmDev *fd) {
+    return emf_tab_bytes(fd->ns, fd->K, fd->r) + (size_t)emf_waves(fd->K) * emf_obw(fd->K);
+}
+
+// 7-bit emission steps when their tables leave the staging room
+bool fsm_k_fits(const hh_fsm_tables *F) {
+    return F->K == 7 && emf_tab_bytes(F->ns, 7, F->r) + emf_waves(7) * emf_obw(7) <= 160u * 1024u;
+}
 
 void fsm_free(FsmDev *fd) {
     if (fd->ct) (void)hipFree(fd->ct);
@@ -737,7 +746,7 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G) {
 }
 
 static int fsm_grids(FsmDev *fd) {
-    if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns) return HH_OK;
+    if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns && fd->sized_K == fd->K) return HH_OK;
     const uint32_t sw = fd->S / 32;
     const kcnt_t kc = kcnt_for(sw, false);
     const kemf_t ke = kemf_for(sw, fd->K, false);
@@ -745,13 +754,14 @@ static int fsm_grids(FsmDev *fd) {
     int pc = 0, pe = 0, ncu = 0, dev = 0;
     FS_OK(hipGetDevice(&dev));
     FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kc, 64 * CW, lds_cnt(fd)));
-    FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, ke, 64 * EW, lds_emf(fd)));
+    FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, ke, 64 * emf_waves(fd->K), lds_emf(fd)));
     FS_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (pc < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
     fd->grid_c = (uint32_t)(pc * ncu);
     fd->grid_e = (uint32_t)(pe * ncu);
     fd->sized_S = fd->S;
     fd->sized_ns = fd->ns;
+    fd->sized_K = fd->K;
     return HH_OK;
 }
 
@@ -830,17 +840,18 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     FS_OK(hipGetLastError());
     FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
+        const uint32_t ew = emf_waves(fd->K);
         // tiles that end before the stream, then the last one(s) (TAIL)
         const uint64_t ne = std::max<uint64_t>(emit_from, std::min<uint64_t>(bits / TB, nt));
         if (ne > emit_from) {
-            const uint64_t nwg = (ne - emit_from + EW - 1) / EW;
+            const uint64_t nwg = (ne - emit_from + ew - 1) / ew;
             const uint32_t ge = (uint32_t)(nwg < fd->grid_e ? nwg : fd->grid_e);
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, false), dim3(ge), dim3(64 * EW), lds_emf(fd), st,
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, false), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne);
             FS_OK(hipGetLastError());
         }
         if (ne < nt) {
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, true), dim3((unsigned)((nt - ne + EW - 1) / EW)), dim3(64 * EW),
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, true), dim3((unsigned)((nt - ne + ew - 1) / ew)), dim3(64 * ew),
                                lds_emf(fd), st, (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt);
             FS_OK(hipGetLastError());
         }

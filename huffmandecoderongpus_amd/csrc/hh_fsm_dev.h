@@ -19,7 +19,7 @@ struct FsmDev {
     uint8_t *tsym;
     uint64_t *et, *er;
     // persistent grids (workgroups), sized by the occupancy API for S / ns
-    uint32_t grid_c, grid_e, sized_S, sized_ns;
+    uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K;
 };
 
 // One decode of tiles [0, ntiles) of the segment at d_data (bits readable
@@ -37,6 +37,7 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
                hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms);
 int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G);
+bool fsm_k_fits(const hh_fsm_tables *F);     // 7-bit emission steps fit beside their staging
 void fsm_free(FsmDev *fd);
 int fsm_debug_arrays(const FsmWs *ws, uint64_t nt, uint32_t *rec, uint32_t *fx, int32_t *tsum, uint32_t *xs);
 

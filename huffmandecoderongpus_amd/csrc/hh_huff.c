@@ -447,7 +447,7 @@ static uint32_t fsm_walk(const hh_tables *T, uint32_t node, uint32_t v, unsigned
     return node;
 }
 
-int hh_fsm_build(const void *tv, uint32_t S, hh_fsm_tables *F) {
+int hh_fsm_build(const void *tv, uint32_t S, uint32_t Kreq, hh_fsm_tables *F) {
     const hh_tables *T = (const hh_tables *)tv;
     /* states: the internal nodes, in compact (BFS) order, root = 0 */
     int32_t *st = (int32_t *)malloc(sizeof(int32_t) * T->tree_used);
@@ -466,7 +466,8 @@ int hh_fsm_build(const void *tv, uint32_t S, hh_fsm_tables *F) {
     if (ns == 0 || st[0] != 0) { rc = HH_ERR_UNSUPPORTED; goto out; }
     memset(F, 0, sizeof(*F));
     F->ns = ns;
-    F->K = T->minlen >= 2 ? 6u : 4u;
+    if (Kreq != 0 && Kreq != 6 && Kreq != 7) { rc = HH_ERR_ARG; goto out; }
+    F->K = T->minlen >= 2 ? (Kreq ? Kreq : 6u) : 4u;
     F->S = S;
     F->r = S % F->K;
     for (uint32_t s = 0; s < ns; s++) {

@@ -206,8 +206,9 @@ def iid_symbols_np(cum: np.ndarray, start: int, n: int, seed: int = IID_SEED) ->
     return np.searchsorted(cum, x, side="right").astype(np.uint8)
 
 
-def code_table(tree) -> tuple[np.ndarray, np.ndarray]:
-    """(code bits LSB-first = first branch in bit 0, code length) per byte."""
+def code_table(tree, max_len: int = 32) -> tuple[np.ndarray, np.ndarray]:
+    """(code bits LSB-first = first branch in bit 0, code length) per byte;
+    encode_gpu takes codes of up to 60 bits."""
     code = np.zeros(256, np.int64)
     L = np.zeros(256, np.int64)
     stack = [(0, 0, 0)]
@@ -220,8 +221,8 @@ def code_table(tree) -> tuple[np.ndarray, np.ndarray]:
         else:
             stack.append((int(tree.izero[v]), d + 1, c))
             stack.append((int(tree.ione[v]), d + 1, c | (1 << d)))
-    if L.max() > 32:
-        raise ValueError("codes longer than 32 bits")
+    if L.max() > max_len:
+        raise ValueError(f"codes longer than {max_len} bits")
     return code, L
 
 
@@ -245,7 +246,8 @@ def encode_gpu(syms, code, lens, device="cuda", chunk: int = 1 << 27):
     """Pack symbols (torch uint8) LSB-first with (code, lens) on the GPU ->
     (payload uint8 tensor with 72 pad bytes, bits).  Codes of distinct
     symbols occupy disjoint bits, so OR is a sum: 32-bit words are built by
-    index_add_ of each code's low and high parts in int64."""
+    index_add_ of each code's parts in int64 (a code of up to 60 bits spans
+    at most three words)."""
     import torch
     codes = torch.as_tensor(code, device=device)
     lt = torch.as_tensor(lens, device=device)
@@ -264,7 +266,9 @@ def encode_gpu(syms, code, lens, device="cuda", chunk: int = 1 << 27):
         cv = codes[s]
         w, sh = pos >> 5, pos & 31
         words.index_add_(0, w, (cv << sh) & 0xffffffff)
-        words.index_add_(0, w + 1, cv >> (32 - sh))
+        words.index_add_(0, w + 1, (cv >> (32 - sh)) & 0xffffffff)
+        if int(lt.max().item()) > 32:
+            words.index_add_(0, w + 2, (cv >> 32) >> (32 - sh))
         del s, ln, pos, cv, w, sh
     payload = words.to(torch.int32).view(torch.uint8)
     return payload, total

@@ -24,10 +24,14 @@
 
 static hh_tables g_T;
 static hh_fsm_tables g_F;
+static uint32_t g_K = 0;                            // emission step bits asked for (hh_fsm_emu_set_k)
 static std::vector<uint32_t> g_rec, g_xs, g_fx;   // the last decode's count-pass arrays
 static std::vector<int64_t> g_tsum;
 
 extern "C" {
+
+// The emission step the next decodes build their tables for (0, 6, 7).
+void hh_fsm_emu_set_k(uint32_t K) { g_K = K; }
 
 // stats[0] tiles  [1] walks  [2] walks not met in their region  [3] S
 // [4] G  [5] next-tile corrections  [6] corrections over > 1 region
@@ -42,7 +46,7 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
     for (int i = 0; i < 9; i++) stats[i] = 0;
     if (S == 0) S = hh_pick_region_bits((uint32_t)g_T.len_gcd);
     if (S < 32 || S % 32) return HH_ERR_ARG;
-    rc = hh_fsm_build(&g_T, S, &g_F);
+    rc = hh_fsm_build(&g_T, S, g_K, &g_F);
     if (rc) return rc;
     uint32_t G = G_req >= 0 ? (uint32_t)G_req : hh_fsm_pick_head(&g_T);
     if (G % 8 || G > 64 || G > S) return HH_ERR_ARG;
@@ -203,7 +207,7 @@ int64_t hh_fsm_emu_tables(const int32_t *izero, const int32_t *ione, const uint8
     hh_tree tree = {nodes, izero, ione, sym};
     int rc = hh_tables_build(&tree, &g_T);
     if (rc) return rc;
-    rc = hh_fsm_build(&g_T, S, &g_F);
+    rc = hh_fsm_build(&g_T, S, g_K, &g_F);
     if (rc) return rc;
     info[0] = g_F.ns;
     info[1] = g_F.K;

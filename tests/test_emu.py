@@ -189,10 +189,13 @@ def femu():
                                                        C.c_void_p]
     L.hh_fsm_emu_tables.restype = C.c_int64
     L.hh_fsm_emu_tables.argtypes = [C.c_void_p] * 3 + [C.c_int32, C.c_uint32, C.c_void_p]
+    L.hh_fsm_emu_set_k.restype = None
+    L.hh_fsm_emu_set_k.argtypes = [C.c_uint32]
     return L
 
 
-def run_femu(L, izero, ione, sym, data, bits, S=0, G=-1, ntiles=0, prologue=0, in_state=0):
+def run_femu(L, izero, ione, sym, data, bits, S=0, G=-1, ntiles=0, prologue=0, in_state=0, K=0):
+    L.hh_fsm_emu_set_k(K)                     # emission step bits (0: the default, 6)
     iz = np.ascontiguousarray(izero, np.int32)
     io = np.ascontiguousarray(ione, np.int32)
     sy = np.ascontiguousarray(sym, np.uint8)
@@ -209,11 +212,13 @@ def run_femu(L, izero, ione, sym, data, bits, S=0, G=-1, ntiles=0, prologue=0, i
 
 @pytest.mark.parametrize("name", ["hello", "paper1", "news", "book2", "kjv.txt", "E.coli",
                                   "world192.txt", "bible.txt"])
-@pytest.mark.parametrize("S", [0, 96])
-def test_fsm_fixtures(femu, name, S):
+@pytest.mark.parametrize("S,K", [(0, 6), (96, 6), (0, 7), (96, 7)])
+def test_fsm_fixtures(femu, name, S, K):
+    """Every fixture, 6- and 7-bit emission steps (7 with 256-bit regions: a
+    4-bit remainder step; with 96: a 5-bit one)."""
     hf = H.HuffFile.load(os.path.join(FILES, name + ".huff"))
     ref = O.OracleHuff.load(os.path.join(FILES, name + ".huff")).chain_decode()
-    n, out, st, _, _ = run_femu(femu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits, S)
+    n, out, st, _, _ = run_femu(femu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits, S, K=K)
     assert n == len(ref) and np.array_equal(out, ref), (n, st)
 
 
@@ -241,11 +246,11 @@ def test_fsm_random_trees_and_tails(femu, seed):
     data, bits = t.encode(text)
     for cut in (bits, bits - 1, max(1, bits // 3 + 1)):   # cut codes exercise the tail rule
         ref = oracle_chain(iz, io, sy, data, cut)
-        for S in (0, 64):
-            n, out, st, _, _ = run_femu(femu, iz, io, sy, data, cut, S)
+        for S, K in ((0, 6), (64, 6), (0, 7)):
+            n, out, st, _, _ = run_femu(femu, iz, io, sy, data, cut, S, K=K)
             if n == UNSUPPORTED:       # a code whose chains never meet (lattice)
                 continue
-            assert n == len(ref) and np.array_equal(out, ref), (cut, S, st)
+            assert n == len(ref) and np.array_equal(out, ref), (cut, S, K, st)
 
 
 def test_fsm_long_codes(femu):
@@ -327,3 +332,10 @@ def test_fsm_tables_shape(femu):
     assert femu.hh_fsm_emu_tables(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), 256,
                                   info.ctypes.data) == 0
     assert list(info) == [83, 6, 4, 64]
+    femu.hh_fsm_emu_set_k(7)
+    try:
+        assert femu.hh_fsm_emu_tables(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), 256,
+                                      info.ctypes.data) == 0
+    finally:
+        femu.hh_fsm_emu_set_k(0)
+    assert list(info) == [83, 7, 4, 64]

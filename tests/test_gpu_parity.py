@@ -33,6 +33,7 @@ def test_fixture_host(hh, dec, files_dir, name):
     out = dec.decode_host(hf.payload, hf.bits, hf.uncompressedsize + 3)
     st = dec.stats()
     assert st["exact_fallback"] == 0
+    assert st["state_machine"] == 1 or st["fixed_length"] == 1     # (E.coli: k_fixed)
     assert len(out) == len(ref) == hf.uncompressedsize
     assert np.array_equal(out, ref)
 
@@ -49,6 +50,7 @@ def test_fixture_device(hh, dec, files_dir, name):
     n = dec.decode_device(d_in, hf.bits, d_out)
     torch.cuda.synchronize()
     assert dec.stats()["exact_fallback"] == 0      # the fast path decoded it
+    assert dec.stats()["state_machine"] == 1 or dec.stats()["fixed_length"] == 1
     assert n == len(ref)
     assert np.array_equal(d_out[:n].cpu().numpy(), ref)
     assert int(d_out[n:].sum().item()) == 0   # nothing written past the end
@@ -620,6 +622,93 @@ def test_non_resynchronising_code_beyond_2_31_bits(hh):
         got = dec.decode_device(payload, bits, out)
         torch.cuda.synchronize()
         assert dec.stats()["exact_fallback"] == 2
+        assert got == n
+        assert torch.equal(out[:n], syms)
+        assert int(out[n:n + 64].ne(0xAB).sum()) == 0
+    finally:
+        dec.close()
+        del out, payload, syms
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("name,mib", [("E.coli", 0), ("E.coli", 1024)])
+def test_state_machine_on_a_fixed_length_code(hh, files_dir, name, mib):
+    """BASELINE config 5's general path: E.coli's 2-bit code with k_fixed
+    off (HH_FLAG_NO_FIXED) goes through the state machine (every region's
+    guess is right, the densest output: 4 symbols per byte).  The fixture
+    against the oracle; the 1 GiB tiled stream (4 GiB of output) against the
+    tiled text."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    dec = hh.Decoder(0, flags=hh.FLAG_NO_FIXED)
+    try:
+        if mib == 0:
+            path = os.path.join(files_dir, name + ".huff")
+            hf = hh.HuffFile.load(path)
+            ref = O.OracleHuff.load(path).chain_decode()
+            dec.set_tree(hf.tree())
+            out = dec.decode_host(hf.payload, hf.bits, hf.uncompressedsize + 3)
+            st = dec.stats()
+            assert st["state_machine"] == 1 and st["fixed_length"] == 0
+            assert np.array_equal(out, ref)
+        else:
+            hf, text = synth.load_source(files_dir, name)
+            syn = synth.tiled_stream(hf, text, mib << 20)
+            dec.set_tree(syn.tree)
+            out = torch.full((syn.decoded_bytes + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+            n = dec.decode_device(syn.data, syn.bits, out)
+            torch.cuda.synchronize()
+            st = dec.stats()
+            assert st["state_machine"] == 1 and st["fixed_length"] == 0
+            assert n == syn.decoded_bytes and synth.verify_tiled(out, syn)
+            assert int(out[n:n + 64].ne(0xAB).sum()) == 0
+            del out, syn
+            torch.cuda.empty_cache()
+    finally:
+        dec.close()
+
+
+def _caterpillar(depth):
+    """Symbol k < depth: k ones then a zero (k + 1 bits); symbol depth:
+    depth ones.  Internal node k holds symbol k as its tail-rule byte."""
+    # node 2k: internal, its zero child 2k+1 a leaf, its one child 2k+2
+    n = 2 * depth + 1
+    izero = np.full(n, -1, np.int32)
+    ione = np.full(n, -1, np.int32)
+    sym = np.zeros(n, np.uint8)
+    for k in range(depth):
+        izero[2 * k], ione[2 * k], sym[2 * k] = 2 * k + 1, 2 * k + 2, k
+        sym[2 * k + 1] = k
+    sym[2 * depth] = depth
+    return izero, ione, sym
+
+
+def test_long_codes_beyond_2_31_bits(hh):
+    """Codes of up to 40 bits (a caterpillar tree: 40 states) through the
+    state machine on a stream of more than 2^31 bits: 110 M symbols drawn
+    uniformly (20.5 bits on average), encoded on the GPU, decoded, compared
+    with the symbols.  Round 2 sent codes over 32 bits to the O(bits log)
+    stage pipeline, capped below 2^31 bits."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    iz, io, sy = _caterpillar(40)
+    tree = hh.Tree(iz, io, sy)
+    code, lens = synth.code_table(tree, max_len=40)
+    assert lens.max() == 40
+    n = 110_000_000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(40)
+    syms = torch.randint(0, 41, (n,), dtype=torch.uint8, device="cuda", generator=g)
+    payload, bits = synth.encode_gpu(syms, code, lens)
+    assert bits > 1 << 31
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(tree)
+        out = torch.full((n + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+        got = dec.decode_device(payload, bits, out)
+        torch.cuda.synchronize()
+        st = dec.stats()
+        assert st["state_machine"] == 1 and st["exact_fallback"] == 0
         assert got == n
         assert torch.equal(out[:n], syms)
         assert int(out[n:n + 64].ne(0xAB).sum()) == 0
