@@ -1875,7 +1875,7 @@ static int decode_fast(hh_decoder *d, const void *d_data, uint64_t bits_avail, u
     d->stats.ms_total = ms[0] + ms[1] + ms[2];
     d->stats.lanes = nt * HH_NR;
     d->stats.out_len = *total;
-    if (fl & F_FAIL) return HH_ERR_UNSUPPORTED;
+    if (fl & F_FAIL) return HH_NOSYNC;
     if (*total > cap || (fl & F_OVER)) return HH_ERR_CAPACITY;
     return HH_OK;
 }
@@ -2003,7 +2003,7 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
         const int rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, d_data, bits, 0, 0, 0, d_out, cap, st,
                                   &total, &leave, &en, ms);
         fsm_stats(d, bits, total, ms);
-        if (rc == HH_ERR_UNSUPPORTED) {
+        if (rc == HH_NOSYNC) {
             // chains that did not meet within HH_FSM_KM regions: a code that
             // does not resynchronise
             d->stats.repairs = 1;
@@ -2029,7 +2029,7 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     uint32_t leave = 0, cp = 0, cs = 0, en = 0;
     int rc = decode_fast(d, d_data, bits, 0, hh_state_pack(0, 0, 0), 0, d_out, cap, st, &total,
                          &leave, &cp, &cs, &en);
-    if (rc == HH_ERR_UNSUPPORTED) {
+    if (rc == HH_NOSYNC) {
         // A walk found no shared boundary within HH_KM regions (a code that
         // does not resynchronise): the segment path, exact and O(N).
         d->stats.exact_fallback = 2;
@@ -2069,6 +2069,7 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
                                   rg->in_state, rg->prologue, d_out, cap, st, &ro->out_len, &ro->leave_state,
                                   &ro->entry_state, ms);
         fsm_stats(d, rg->bits_avail, ro->out_len, ms);
+        if (rc == HH_NOSYNC) return HH_ERR_UNSUPPORTED;   // (decode such a code whole)
         // the state leaving a segment does not depend on how it was entered
         // once the chains have met inside it; the entry after a prologue is
         // checked against the predecessor's leave state by the caller
@@ -2084,7 +2085,7 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
                                d_out, cap, st, &ro->out_len, &ro->leave_state, &cp,
                                &ro->const_seen, &ro->entry_state);
     ro->entry_exact = rg->prologue == 0 || cp != 0;
-    return rc;
+    return rc == HH_NOSYNC ? HH_ERR_UNSUPPORTED : rc;
 }
 
 // evaluate() scope (decodeUtil.c:41-43 times the whole decoder call): host
@@ -2108,7 +2109,12 @@ static void par_memcpy(uint8_t *dst, const uint8_t *src, size_t len) {
     const size_t part = (len / nt + 4095) & ~(size_t)4095;
     for (size_t i = 1; i < nt; i++) {
         const size_t o = i * part;
-        if (o < len) th[i] = std::thread(memcpy, dst + o, src + o, std::min(part, len - o));
+        if (o >= len) continue;
+        try {
+            th[i] = std::thread(memcpy, dst + o, src + o, std::min(part, len - o));
+        } catch (...) {   // (no thread to be had: this part on the calling thread)
+            memcpy(dst + o, src + o, std::min(part, len - o));
+        }
     }
     memcpy(dst, src, std::min(part, len));
     for (size_t i = 1; i < nt; i++)
@@ -2223,7 +2229,7 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
     if (cap) (void)hipHostUnregister(out);
     fsm_stats(d, bits, total, ms_all);
     *out_len = total;
-    return rc;
+    return rc == HH_NOSYNC ? HH_ERR_UNSUPPORTED : rc;   // (no resync: the serial path decodes it whole)
 }
 
 extern "C" int hh_decode_host(hh_decoder *d, const uint8_t *data, uint64_t bits, uint8_t *out,

@@ -867,7 +867,7 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
     (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
     (void)hipEventElapsedTime(&ms[2], ev[2], ev[3]);
-    if (fl & FF_FAIL) return HH_ERR_UNSUPPORTED;
+    if (fl & FF_FAIL) return HH_NOSYNC;
     if (*total > cap || (fl & FF_OVER)) return HH_ERR_CAPACITY;
     return HH_OK;
 }

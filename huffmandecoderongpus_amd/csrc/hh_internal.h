@@ -58,10 +58,20 @@
 #endif
 #define HH_L1_SIZE (1u << HH_P)
 #ifndef HH_PF
-#define HH_PF 13                /* F index bits (11 <= HH_PF <= 13; 13:
+#define HH_PF 13                /* F index bits (HH_P <= HH_PF <= 13; 13:
                                    11.0 bits per lookup on kjv, 12: 10.1) */
 #endif
+/* an F entry packs nbits and the start mask into 4 + 12 bits, and a code that
+ * escapes F must also escape L1 (its fdir word is an L1 escape word) */
+#if HH_PF < HH_P || HH_PF > 13
+#error "HH_PF must lie in [HH_P, 13]"
+#endif
 #define HH_F_SIZE (1u << HH_PF)
+/* Internal status (never returned through the C ABI): chains that did not
+ * meet within the bounded walk -- a code that does not resynchronise; the
+ * callers fall back to the exact segment path.  Configuration failures keep
+ * their own codes and propagate. */
+#define HH_NOSYNC (-100)
 #define HH_Q_MAX 9              /* max L2 subtable index bits         */
 #define HH_L2_MAX 4096          /* L2 entries kept (LDS budget 16 KB) */
 #define HH_TREE_MAX 32767       /* compact nodes (15-bit ids)         */

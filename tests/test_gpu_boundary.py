@@ -37,18 +37,45 @@ def test_reference_harness_evaluates_hip_plugin():
     assert "different" not in r.stdout
 
 
+@pytest.fixture(scope="module")
+def full_files(tmp_path_factory):
+    """files/ plus the regenerated kjv.txt and E.coli originals (sha256-checked,
+    tools/regen_files.py), so the CLI byte-compares every decode."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import regen_files
+    return regen_files.regen(str(tmp_path_factory.mktemp("files_full")))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("test,name", [("hello", "hello"), ("kjvprof", "kjv")])
-def test_cli_prints_the_reference_line(test, name):
+def test_cli_prints_the_reference_line(test, name, full_files):
     if not os.path.exists(CLI):
         pytest.skip("build/HuffFramework not built")
-    env = dict(os.environ, HIPHUFF_FILES=FILES)
-    # (kjv.txt is absent from the reference tree: the CLI checks the decoded
-    # length against the header then, as its "note:" line says)
+    env = dict(os.environ, HIPHUFF_FILES=full_files)
     r = subprocess.run([CLI, test, "--reps", "3"], capture_output=True, text=True, env=env,
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+    assert "absent" not in r.stderr                   # byte-compared, not length-checked
     assert re.search(LINE.format(dec="hip", name=name), r.stdout, re.M), r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("test,n_min", [("quickgraph2", 20), ("graph2", 40)])
+def test_cli_graphtest_byte_checked(test, n_min, full_files):
+    """graphtest (framework/mainrun.c:387-410): every prefix cut at a symbol
+    boundary (setTargetSizes, mainrun.c:361-385) is decoded and byte-compared
+    with the original's prefix (exit status 1 on a mismatch); kjv.txt is the
+    regenerated original, so graph2 is checked byte for byte too."""
+    if not os.path.exists(CLI):
+        pytest.skip("build/HuffFramework not built")
+    r = subprocess.run([CLI, test, "--files", full_files, "--reps", "1"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "absent" not in r.stderr
+    rows = [ln.split() for ln in r.stdout.splitlines() if re.match(r"^\s*\d+\s+\d+\.\d{9}$", ln)]
+    assert len(rows) >= n_min, r.stdout[-2000:]
+    sizes = [int(x[0]) for x in rows]
+    assert sizes == sorted(sizes) and len(set(sizes)) == len(sizes)
 
 
 def _jacobi_calcbitsindex(levels, bits, nsteps):

@@ -20,6 +20,6 @@ timeout -k 10 600 python3 bench.py > $E/${TAG}_bench_latest.json 2> $E/bench.err
 cat $E/${TAG}_bench_latest.json
 echo "[$(date +%T)] sweep"
 timeout -k 10 600 python3 -u tools/sweep.py $E/${TAG}_size_sweep.json > $E/sweep.log 2>&1 || { tail -20 $E/sweep.log; exit 1; }
-timeout -k 10 120 build/HuffFramework graph2 --files files > $E/${TAG}_graph2_hip.txt 2> $E/graph2.err || exit 1
+timeout -k 10 120 build/HuffFramework graph2 --files $(python3 tools/regen_files.py gpurun_out/files_full) > $E/${TAG}_graph2_hip.txt 2> $E/graph2.err || exit 1
 timeout -k 10 120 build/HuffFramework quickgraph2 --files files > $E/${TAG}_quickgraph2_hip.txt 2>> $E/graph2.err || exit 1
 echo "[$(date +%T)] done"
