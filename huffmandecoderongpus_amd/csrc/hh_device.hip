@@ -1577,10 +1577,11 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     uint32_t Kf = getenv("HH_FSM_K") ? (uint32_t)atoi(getenv("HH_FSM_K")) : 0u;
     if (!Kf && d->S && hh_fsm_build(d->ht, d->S, 7, d->ft) == HH_OK && fsm_k_fits(d->ft)) Kf = 7;
     if (d->S && hh_fsm_build(d->ht, d->S, Kf ? Kf : 6, d->ft) == HH_OK) {
-        uint32_t Gf = hh_fsm_pick_head(d->ht);
+        uint32_t Gf = hh_fsm_pick_head(d->ht, d->S);
         if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) & ~7u;   // experiments
         if (Gf > d->S) Gf = 0;
         const int urc = fsm_upload(&d->fsm, d->ft, Gf);
+        d->fsm.dbg = d->d_dbg;
         if (urc != HH_OK && urc != HH_ERR_UNSUPPORTED) return urc;
     }
     d->have_tree = 1;

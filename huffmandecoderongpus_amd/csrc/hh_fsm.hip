@@ -44,18 +44,25 @@
     } while (0)
 
 #define NR 64                 // regions per tile (a wave)
-#define CW 8                  // k_cnt: waves per workgroup
-// k_emf: waves per workgroup and output staging per wave (bytes) -- 7-bit
-// steps leave less room beside their tables (a kjv tile's output is ~1.8 KB
-// on average)
-#ifndef HH_EMF7_WAVES
-#define HH_EMF7_WAVES 12
+#ifndef HH_CW
+#define HH_CW 12
 #endif
-#ifndef HH_EMF7_OBW
-#define HH_EMF7_OBW 5120
+#define CW HH_CW               // k_cnt: waves per workgroup
+#ifndef HH_CNT_PNX
+#define HH_CNT_PNX 0          // k_cnt: region j+1's words prefetched a tile ahead (1) or loaded at a walk (0)
 #endif
-__host__ __device__ constexpr uint32_t emf_waves(uint32_t K) { return K == 7 ? HH_EMF7_WAVES : 16u; }
-__host__ __device__ constexpr uint32_t emf_obw(uint32_t K) { return K == 7 ? HH_EMF7_OBW : 6144u; }
+#ifndef HH_WALK_MASK
+#define HH_WALK_MASK 1        // k_cnt walks: only the lanes not met yet look up
+#endif
+#ifndef HH_WALK_CHK
+#define HH_WALK_CHK 1         // k_cnt walks: ask whether every lane has met every HH_WALK_CHK + 1 steps
+#endif
+// k_emf: waves per workgroup (at most; the active ones are sized at run time)
+// for NCH chains per lane -- two chains need the register room of 12 waves
+#ifndef HH_EMF2_WAVES
+#define HH_EMF2_WAVES 12
+#endif
+__host__ __device__ constexpr uint32_t emf_waves(uint32_t nch) { return nch == 2 ? HH_EMF2_WAVES : 16u; }
 #define SCAN_TB 1024          // tiles per k_fscan1 block
 #define FX_W 8                // corrections per tile (HH_FSM_KM)
 static_assert(FX_W == HH_FSM_KM, "corrections per tile");
@@ -75,14 +82,31 @@ struct FsmGeo {
 
 // Workspace (fsm_decode).  Nothing needs zeroing but `flags`.
 struct FsmWork {
-    uint32_t *flags;      // [0] status, [2..3] total, [4] leave state, [5] entry state
+    uint32_t *flags;      // [0] status, [2..3] total, [4] leave state, [5] entry state,
+                          // [6] the largest tile output
     uint32_t *rec;        // [ntiles][NR] entering state | count << 8
     int32_t *tsum;        // [ntiles] the tile's count (its own view of region 0)
     uint32_t *xs;         // [ntiles] the state leaving the tile
     uint32_t *fx;         // [ntiles + 1][FX_W] corrections of a tile's first regions
     int32_t *lex;         // [ntiles + 1] exclusive prefix within the scan block
     int64_t *blk;         // [nblk] block totals, then block bases
+    int32_t *bmax;        // [nblk] the block's largest tile count (k_emf sizes its staging by it)
+    uint64_t *dbg;        // HH_DIAG builds: [0..3] k_cnt phase cycles (head, count, walks, records),
+                          // [8] tiles, [9] tiles with a walk, [10] walk rounds
 };
+
+#ifdef HH_DIAG
+#define CDIAG_DECL uint64_t cg_acc[4] = {0, 0, 0, 0}, cg_n[3] = {0, 0, 0}; uint64_t cg_t = __builtin_amdgcn_s_memtime();
+#define CDIAG_STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); cg_acc[i] += t_ - cg_t; cg_t = t_; } while (0)
+#define CDIAG_COUNT(i, v) do { cg_n[i] += (v); } while (0)
+#define CDIAG_FLUSH(dbg) do { if ((threadIdx.x & 63u) == 0) { for (int i_ = 0; i_ < 4; i_++) atomicAdd((unsigned long long *)&(dbg)[i_], (unsigned long long)cg_acc[i_]); \
+    for (int i_ = 0; i_ < 3; i_++) atomicAdd((unsigned long long *)&(dbg)[8 + i_], (unsigned long long)cg_n[i_]); } } while (0)
+#else
+#define CDIAG_DECL
+#define CDIAG_STAMP(i) do {} while (0)
+#define CDIAG_COUNT(i, v) do {} while (0)
+#define CDIAG_FLUSH(dbg) do {} while (0)
+#endif
 
 struct FsmTab {
     const uint16_t *ct;
@@ -215,7 +239,10 @@ __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_
 
 // Walk: chains A and B stepped together over a region until they meet
 // (their count difference stops changing then); lanes not walking carry
-// A == B.  Stops when every lane has met.
+// A == B.  Only the lanes whose chains have not met yet look up (the others
+// are masked off: a table read costs LDS cycles per distinct bank address of
+// its ACTIVE lanes, and most lanes do not walk).  Stops when every lane has
+// met.
 template <uint32_t SW, bool TAIL>
 __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
                                             uint32_t &A, uint32_t &B, int32_t &d, uint32_t lim) {
@@ -223,13 +250,15 @@ __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *
 #pragma unroll
     for (uint32_t k = 0; k < 4 * SW; k++) {
         if (go && (!TAIL || 8 * k + 8 <= lim)) {
-            const uint32_t x = rbyte<SW>(w, k);
-            const uint32_t ea = ct_at(lds, A, x), eb = ct_at(lds, B, x);
-            A = ea & 0xfe00u;
-            B = eb & 0xfe00u;
-            d += (int32_t)(ea & 15u) - (int32_t)(eb & 15u);
+            if (!HH_WALK_MASK || A != B) {
+                const uint32_t x = rbyte<SW>(w, k);
+                const uint32_t ea = ct_at(lds, A, x), eb = ct_at(lds, B, x);
+                A = ea & 0xfe00u;
+                B = eb & 0xfe00u;
+                d += (int32_t)(ea & 15u) - (int32_t)(eb & 15u);
+            }
         }
-        if ((k & 3) == 3 && go) go = __ballot(A != B) != 0;
+        if ((k & HH_WALK_CHK) == HH_WALK_CHK && go) go = __ballot(A != B) != 0;
     }
     if (TAIL) {
         for (uint32_t q = lim & ~7u; q < lim && A != B; q++) {
@@ -252,11 +281,20 @@ __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns) {
 }
 
 // One tile: w = region j's words, nx = region j+1's (lane 63: the next
-// tile's region 0).
+// tile's region 0), or (HH_CNT_PNX == 0) loaded here when some lane walks --
+// with a 128-bit head most tiles have no walk, and registers held across the
+// count for the rare walk cost occupancy.
+#ifdef HH_DIAG
+#define CDIAG_ARGS , uint64_t *cg_acc, uint64_t *cg_n, uint64_t &cg_t
+#define CDIAG_PASS , cg_acc, cg_n, cg_t
+#else
+#define CDIAG_ARGS
+#define CDIAG_PASS
+#endif
 template <uint32_t SW, bool TAIL>
 __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
                                          const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
-                                         const uint32_t *nx) {
+                                         const uint32_t *nx CDIAG_ARGS) {
     constexpr uint32_t S = 32 * SW;
     const uint32_t j = threadIdx.x & 63u;
     const uint64_t TB = (uint64_t)NR * S, T0 = t * TB;
@@ -272,15 +310,18 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     // decodeallbits: the guess for region j+1 (a chain started at the root G
     // bits before it), then region j from the guess lane j-1 made for it
     uint32_t gs = 0;
-    if (geo.G) {
-        const uint32_t GB = geo.G >> 3;
+#ifndef HH_XP_NOHEAD
+#define HH_XP_NOHEAD 0        // (timing experiments only: results are wrong)
+#endif
+    if (geo.G && !HH_XP_NOHEAD) {
+        const uint32_t GB = geo.G >> 3;                   // (uniform)
+        constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
 #pragma unroll
-        for (uint32_t k = 4 * SW - 8; k < 4 * SW; k++) {
-            gs = k == 4 * SW - GB ? 0u : gs;
-            gs = ct_at(lds, gs, rbyte<SW>(w, k));
-        }
+        for (uint32_t k = 4 * SW - HB; k < 4 * SW; k++)
+            if (k >= 4 * SW - GB) gs = ct_at(lds, gs, rbyte<SW>(w, k));
         gs &= 0xfe00u;
     }
+    CDIAG_STAMP(0);
     const uint32_t gup = shfl_up1(gs);              // (cross-lane ops with every lane active)
     const uint32_t sp = j ? gup : (t == 0 ? geo.in_state << 9 : 0u);
     uint32_t n;
@@ -290,6 +331,7 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     const bool endj = TAIL && lim > 0 && R + lim == geo.bits;
     const bool endn = TAIL && limn > 0 && R + S + limn == geo.bits;
     if (endj && X != 0) n += 1;
+    CDIAG_STAMP(1);
 
     // makebigtable: where region j's exit differs from the entry assumed for
     // region j+1 (E), lane j walks region j+1 with both chains; their count
@@ -300,17 +342,29 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     uint32_t E = j == 63 ? 0u : gs;
     int32_t d = 0;
     bool lost = false;                              // lane 63: not met in the next tile's region 0
-    for (int round = 0; round < NR; round++) {
+#ifndef HH_XP_NOWALK
+#define HH_XP_NOWALK 0        // (timing experiments only: results are wrong)
+#endif
+    uint32_t nv[SW];
+    for (int round = 0; round < (HH_XP_NOWALK ? 0 : NR); round++) {
         const bool want = X != E && limn > 0 && (j < 63 || has_next);
         if (__ballot(want) == 0) break;
+        CDIAG_COUNT(1, round == 0);
+        CDIAG_COUNT(2, 1);
         uint32_t A = X, B = want ? E : X;           // (not walking: A == B, no change)
         int32_t dd = 0;
-        uint32_t nv[SW];
+        if (round == 0) {
+            if (HH_CNT_PNX) {
 #pragma unroll
-        for (uint32_t k = 0; k < SW; k++) {
-            nv[k] = nx[k];
-            asm volatile("" : "+v"(nv[k]));
+                for (uint32_t k = 0; k < SW; k++) nv[k] = nx[k];
+            } else {
+                fs_load<SW>(nv, fs_rsrc(g, uni64(t) * TB / 32, geo.nwords), (j + 1) * SW);
+            }
         }
+        // (opaque per round: the byte offsets of the walk are not hoisted out
+        // of the rounds loop into 4 x SW live registers)
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) asm volatile("" : "+v"(nv[k]));
         walk_region<SW, TAIL>(lds, F.b1, nv, A, B, dd, limn);
         bool deep = false;
         if (want) {
@@ -327,6 +381,8 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
         if (j > 0 && dp) X = xa;
     }
 
+    CDIAG_STAMP(2);
+    CDIAG_COUNT(0, 1);
     // records: region j entered in the state lane j-1 assumed last
     const uint32_t Eup = shfl_up1(E), dup = shfl_up1((uint32_t)d);
     const uint32_t ent = (j ? Eup : sp) >> 9;
@@ -354,10 +410,11 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
             for (int i = 0; i < FX_W; i++) wk.fx[(t + 1) * FX_W + i] = f[i];
         }
     }
+    CDIAG_STAMP(3);
 }
 
 #ifndef HH_CNT_WAVES
-#define HH_CNT_WAVES 4        // k_cnt: waves per SIMD the register budget is cut for
+#define HH_CNT_WAVES 6        // k_cnt: waves per SIMD the register budget is cut for (24 per CU: 2 workgroups of 12)
 #endif
 template <uint32_t SW, bool TAIL>
 __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
@@ -375,22 +432,30 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts};
     const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * CW;
     uint64_t t = t0 + (uint64_t)blockIdx.x * CW + wv;
-    // the next tile's region words are loaded one tile ahead; region j+1's
-    // (used only by walks, well after the count) at the tile's start
-    uint32_t pw[SW];
+    // the next tile's words are loaded one tile ahead: region j's and region
+    // j+1's (used only by walks; waiting for them at the walk, behind the
+    // previous tile's stores, cost as much as the walks themselves)
+    uint32_t pw[SW], pn[SW] = {};
     auto prefetch = [&](uint64_t tt) {
         tt = uni64(tt);
-        fs_load<SW>(pw, fs_rsrc(g, tt * TB / 32, geo.nwords), j * SW);
+        const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
+        fs_load<SW>(pw, rs, j * SW);
+        if (HH_CNT_PNX) fs_load<SW>(pn, rs, (j + 1) * SW);
     };
+    CDIAG_DECL
     if (t < t1) prefetch(t);
     for (; t < t1; t += nwv) {
         uint32_t w[SW], nx[SW];
 #pragma unroll
-        for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
-        fs_load<SW>(nx, fs_rsrc(g, uni64(t) * TB / 32, geo.nwords), (j + 1) * SW);
+        for (uint32_t k = 0; k < SW; k++) {
+            w[k] = pw[k];
+            nx[k] = pn[k];
+        }
+        if (!HH_CNT_PNX) fs_load<SW>(nx, fs_rsrc(g, uni64(t) * TB / 32, geo.nwords), (j + 1) * SW);
         prefetch(t + nwv < t1 ? t + nwv : t);
-        cnt_tile<SW, TAIL>(smem, F, g, geo, wk, t, w, nx);
+        cnt_tile<SW, TAIL>(smem, F, g, geo, wk, t, w, nx CDIAG_PASS);
     }
+    CDIAG_FLUSH(wk.dbg);
 }
 
 // ---------------------------------------------------------------------------
@@ -400,7 +465,7 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
 // the corrections its predecessor wrote; prologue tiles emit nothing), the
 // exclusive prefix within the block -> lex, the block total -> blk.
 __global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk) {
-    __shared__ int32_t s_tmp[SCAN_TB / 64];
+    __shared__ int32_t s_tmp[SCAN_TB / 64], s_mx[SCAN_TB / 64];
     const uint64_t t = (uint64_t)blockIdx.x * SCAN_TB + threadIdx.x;
     int32_t c = 0;
     if (t < geo.ntiles && t >= geo.emit_from) {
@@ -410,26 +475,37 @@ __global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk) {
     }
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const int32_t x = wave_incl_scan(c);
+    int32_t m = c;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
     if (lane == 63) s_tmp[wv] = x;
+    if (lane == 0) s_mx[wv] = m;
     __syncthreads();
-    int32_t base = 0, tot = 0;
+    int32_t base = 0, tot = 0, mx = 0;
 #pragma unroll
     for (uint32_t i = 0; i < SCAN_TB / 64; i++) {
         const int32_t v = s_tmp[i];
         base += i < wv ? v : 0;
         tot += v;
+        mx = max(mx, s_mx[i]);
     }
     if (t <= geo.ntiles) wk.lex[t] = base + x - c;
-    if (threadIdx.x == 0) wk.blk[blockIdx.x] = tot;
+    if (threadIdx.x == 0) {
+        wk.blk[blockIdx.x] = tot;
+        wk.bmax[blockIdx.x] = mx;
+    }
 }
 
 // One block: block totals -> exclusive block bases; totals and states.
 __global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_t nblk) {
     __shared__ int64_t s_w[16];
+    __shared__ int32_t s_mx[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     int64_t carry = 0;
+    int32_t mx = 0;
     for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
         const int64_t v = b0 + tid < nblk ? wk.blk[b0 + tid] : 0;
+        if (b0 + tid < nblk) mx = max(mx, wk.bmax[b0 + tid]);
         int64_t x = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -447,7 +523,13 @@ __global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_
         carry += tot;
         __syncthreads();
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) s_mx[wv] = mx;
+    __syncthreads();
     if (tid == 0) {
+        for (uint32_t i = 0; i < 16; i++) mx = max(mx, s_mx[i]);
+        wk.flags[6] = (uint32_t)mx;       // the largest tile output (symbols)
         wk.flags[2] = (uint32_t)carry;
         wk.flags[3] = (uint32_t)((uint64_t)carry >> 32);
         wk.flags[4] = geo.ntiles ? wk.xs[geo.ntiles - 1] : geo.in_state;
@@ -467,26 +549,26 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
     return ((ns << K) * 8u + (r ? (ns << r) * 8u : 0u) + ns * 8u + ns + 15u) & ~15u;
 }
 
-// Region j entered in state s, its symbols to the staging from LDS byte
-// address oa on: K-bit steps, each step's symbols shifted into the current
-// dword, which is stored to its aligned LDS address every step (a dword is
-// stored again until it is full: no branch), then the r-bit step (r = S mod
-// K); TAIL: steps while whole, the rest bit by bit, and the tail rule.  The
+// The emission chain of one region (state, output dword, shift) while it
+// stores each step's symbols into the staging: every step's symbols are
+// shifted into the current dword, which is stored to its aligned LDS address
+// every step (a dword is stored again until it is full: no branch).  The
 // unused bytes of every stored dword are zero: a dword shared with the
-// neighbouring runs is repaired by OR afterwards (emf_edges).  *first: the
-// run's bytes in its first dword (valid when *first_ok), *lastw / *lastwd:
-// the run's last dword.
+// neighbouring runs is repaired by OR afterwards (emf_edges).
 #define EMF_KE 8          // steps within which the first dword is captured
-template <uint32_t SW, uint32_t K, bool TAIL>
-__device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const uint32_t *b1, const uint8_t *ts,
-                                           const uint32_t *w, uint32_t s, uint32_t lim, bool at_end, uint32_t oa,
-                                           uint32_t *first, bool *first_ok, uint32_t *lastw, uint32_t *lastwd) {
-    constexpr uint32_t S = 32 * SW, r = S % K;
-    uint32_t row = s << (K + 3);
-    const uint32_t wd0 = oa & ~3u;
-    uint32_t wd = wd0, sh = (oa & 3u) * 8u;
-    uint32_t a = 0;                                 // the current dword's bytes so far
-    auto put = [&](uint64_t e) -> uint32_t {
+template <uint32_t K>
+struct EmfChain {
+    uint32_t row, wd0, wd, sh, a, fw, wdk;
+    __device__ __forceinline__ void init(uint32_t s, uint32_t oa) {
+        row = s << (K + 3);
+        wd0 = oa & ~3u;
+        wd = wd0;
+        sh = (oa & 3u) * 8u;
+        a = 0;                                      // the current dword's bytes so far
+        fw = 0;
+        wdk = wd0;
+    }
+    __device__ __forceinline__ uint32_t put(uint8_t *lds, uint64_t e) {
         const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
         const uint32_t u = sh + (hi & 255u);          // 8 x the symbols: one SDWA add
         // the bytes that do not fit the current dword spill into the next;
@@ -501,43 +583,74 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
         wd += full ? 4u : 0u;
         sh = u & 31u;
         return an;
-    };
-    uint32_t fw = 0, wdk = wd0;
+    }
+    // step k's entry e: store its symbols, capture the first dword, advance
+    __device__ __forceinline__ void step(uint8_t *lds, uint64_t e, uint32_t k) {
+        const uint32_t at = wd;
+        const uint32_t v = put(lds, e);
+        if (k < EMF_KE) fw = at == wd0 ? v : fw;     // the last value stored to the first dword
+        row = HH_FSM_ET_ROW(e);
+        if (k + 1 == EMF_KE) wdk = wd;
+    }
+};
+
+// NCH independent regions (one per chain: region j of NCH tiles) entered in
+// states s[c], their symbols to the staging from LDS byte address oa[c] on:
+// K-bit steps, the NCH chains' table reads issued together (each chain is a
+// dependent sequence of LDS reads; interleaving them hides the latency), then
+// the r-bit step (r = S mod K); TAIL (NCH = 1): steps while whole, the rest
+// bit by bit, and the tail rule.  *first: the run's bytes in its first dword
+// (valid when *first_ok), *lastw / *lastwd: the run's last dword.
+template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH>
+__device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const uint32_t *b1, const uint8_t *ts,
+                                           const uint32_t (*w)[SW], const uint32_t *s, uint32_t lim,
+                                           const bool *at_end, const uint32_t *oa, uint32_t *first, bool *first_ok,
+                                           uint32_t *lastw, uint32_t *lastwd) {
+    constexpr uint32_t S = 32 * SW, r = S % K;
+    EmfChain<K> ch[NCH];
+#pragma unroll
+    for (uint32_t c = 0; c < NCH; c++) ch[c].init(s[c], oa[c]);
 #pragma unroll
     for (uint32_t k = 0; k < S / K; k++) {
         const uint32_t q = k * K;
         if (!TAIL || q + K <= lim) {
-            const uint64_t e = *(const uint64_t *)(lds + row + win8<SW, K>(w, q));
-            const uint32_t at = wd;
-            const uint32_t v = put(e);
-            if (k < EMF_KE) fw = at == wd0 ? v : fw;       // the last value stored to the first dword
-            row = HH_FSM_ET_ROW(e);
+            uint64_t e[NCH];
+#pragma unroll
+            for (uint32_t c = 0; c < NCH; c++) e[c] = *(const uint64_t *)(lds + ch[c].row + win8<SW, K>(w[c], q));
+#pragma unroll
+            for (uint32_t c = 0; c < NCH; c++) ch[c].step(lds, e[c], k);
+        } else if (k + 1 == EMF_KE) {
+#pragma unroll
+            for (uint32_t c = 0; c < NCH; c++) ch[c].wdk = ch[c].wd;
         }
-        if (k + 1 == EMF_KE) wdk = wd;
     }
-    if (!TAIL) {
-        if (r) {
-            const uint64_t e = *(const uint64_t *)(lds + er_off + (row >> (K - r)) + (rbits<SW>(w, S - r, r) << 3));
-            put(e);
-            row = HH_FSM_ET_ROW(e);
+#pragma unroll
+    for (uint32_t c = 0; c < NCH; c++) {
+        EmfChain<K> &x = ch[c];
+        if (!TAIL) {
+            if (r) {
+                const uint64_t e = *(const uint64_t *)(lds + er_off + (x.row >> (K - r)) + (rbits<SW>(w[c], S - r, r) << 3));
+                x.put(lds, e);
+                x.row = HH_FSM_ET_ROW(e);
+            }
+        } else {
+            uint32_t st = x.row >> (K + 3);
+            for (uint32_t q = lim / K * K; q < lim; q++) {
+                const uint32_t v = b1[st * 2 + rbit_dyn<SW>(w[c], q)];
+                st = v & 255u;
+                x.put(lds, HH_FSM_ET_MAKE((v >> 16) & 255u, 0u, (v >> 8) & 255u));
+            }
+            x.row = st << (K + 3);
         }
-    } else {
-        uint32_t st = row >> (K + 3);
-        for (uint32_t q = lim / K * K; q < lim; q++) {
-            const uint32_t v = b1[st * 2 + rbit_dyn<SW>(w, q)];
-            st = v & 255u;
-            put(HH_FSM_ET_MAKE((v >> 16) & 255u, 0u, (v >> 8) & 255u));
-        }
-        row = st << (K + 3);
+        if (at_end[c] && (x.row >> (K + 3)) != 0) x.put(lds, HH_FSM_ET_MAKE(ts[x.row >> (K + 3)], 0u, 1u));   // the tail rule
+        *(uint32_t *)(lds + x.wd) = x.a;               // the bytes of the last step's overflow
+        // the first dword: complete in fw once the run left it within EMF_KE
+        // steps; the final dword when the run never left it
+        first[c] = x.wd == x.wd0 ? x.a : x.fw;
+        first_ok[c] = x.wd == x.wd0 || x.wdk != x.wd0 || (S / K < EMF_KE);
+        lastw[c] = x.a;
+        lastwd[c] = x.wd;
     }
-    if (at_end && (row >> (K + 3)) != 0) put(HH_FSM_ET_MAKE(ts[row >> (K + 3)], 0u, 1u));   // the tail rule
-    *(uint32_t *)(lds + wd) = a;                     // the bytes of the last step's overflow
-    // the first dword: complete in fw once the run left it within EMF_KE
-    // steps; the final dword when the run never left it
-    *first = wd == wd0 ? a : fw;
-    *first_ok = wd == wd0 || wdk != wd0 || (S / K < EMF_KE);
-    *lastw = a;
-    *lastwd = wd;
 }
 
 // After every lane's stores: the dwords a run shares with its neighbours hold
@@ -580,9 +693,17 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
     if (at_end && s != 0) dst[o] = ts[s];
 }
 
-template <uint32_t SW, uint32_t K, bool TAIL>
-__global__ __launch_bounds__(64 * emf_waves(K)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
-                                                 uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1) {
+// k_emf: emission of tiles [t0, t1).  Each wave takes NCH tiles at a time
+// (tiles t, t + W, ..., W = the grid's active waves), one region of each per
+// lane.  The staging is sized from the largest tile output of this decode
+// (flags[6], k_fscan2): as many waves of the workgroup are active as the
+// LDS beside the tables holds NCH tile stagings for (up to EW), so that
+// typical streams keep more chains in flight than a worst-case size allows.
+template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH>
+__global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+                                                 uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1,
+                                                 uint32_t lds_bytes) {
+    static_assert(!TAIL || NCH == 1, "the tail tiles take one chain per lane");
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW;
     const uint32_t ns = geo.ns, r = geo.r, tid = threadIdx.x, j = tid & 63u;
@@ -590,85 +711,114 @@ __global__ __launch_bounds__(64 * emf_waves(K)) void k_emf(const uint32_t *__res
     const uint32_t er_off = (ns << K) * 8u;
     uint32_t *s_b1 = (uint32_t *)(smem + er_off + (r ? (ns << r) * 8u : 0u));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
-    constexpr uint32_t EW = emf_waves(K), OBW = emf_obw(K);
-    const uint32_t stage = emf_tab_bytes(ns, K, r) + wv * OBW;           // the wave's staging (LDS byte address)
+    constexpr uint32_t EW = emf_waves(NCH);
     for (uint32_t i = tid; i < (ns << K); i += blockDim.x) ((uint64_t *)smem)[i] = tab.et[i];
     for (uint32_t i = tid; r && i < (ns << r); i += blockDim.x) ((uint64_t *)(smem + er_off))[i] = tab.er[i];
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
     __syncthreads();
+    // staging per tile: the largest tile output + its 16-B misalignment + the
+    // last step's overflow dword; the active waves share the rest of the LDS
+    const uint32_t tabb = emf_tab_bytes(ns, K, r);
+    const uint32_t pool = lds_bytes > tabb ? lds_bytes - tabb : 0u;
+    const uint32_t mx = __builtin_amdgcn_readfirstlane((int)wk.flags[6]);
+    const uint32_t need = (mx + 16u + 8u + 15u) & ~15u;
+    uint32_t nact = pool / (NCH * need);
+    nact = nact > EW ? EW : nact < 1u ? 1u : nact;
+    if (nact > blockDim.x / 64u) nact = blockDim.x / 64u;
+    if (wv >= nact) return;                          // (no workgroup barrier after this point)
+    const uint32_t obw = pool / (NCH * nact) & ~15u;
 
-    const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * EW;
-    // next tile's words, record, correction and base, loaded one tile ahead
-    // (the base words by lanes 0..2, read out with readlane where consumed)
-    uint32_t pw[SW], prec = 0, pfx = 0, pmeta = 0;
-    auto prefetch = [&](uint64_t tt) {
-        tt = uni64(tt);
-        const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
-        prec = wk.rec[tt * NR + j];
-        pfx = wk.fx[tt * FX_W + (j & (FX_W - 1))];
-        const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / SCAN_TB);
-        const uint32_t ln = j & 3u;
-        pmeta = *(ln == 0 ? blk32 : ln == 1 ? blk32 + 1 : (const uint32_t *)&wk.lex[tt]);
-        fs_load<SW>(pw, rs, j * SW);
-    };
-    uint64_t t = t0 + (uint64_t)blockIdx.x * EW + wv;
-    if (t < t1) prefetch(t);
-    for (; t < t1; t += nwv) {
-        uint32_t w[SW];
+    const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * nact;
+    // next tiles' words, records, corrections and bases, loaded one step
+    // ahead (the base words by lanes 0..2, read out with readlane where consumed)
+    uint32_t pw[NCH][SW], prec[NCH], pfx[NCH], pmeta[NCH];
+    auto prefetch = [&](uint64_t tt0) {
 #pragma unroll
-        for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
-        const uint32_t rc = prec, fx = j < FX_W ? pfx : 0u;
-        const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)pmeta, 0);
-        const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)pmeta, 1);
-        const int32_t lx = __builtin_amdgcn_readlane((int)pmeta, 2);
-        prefetch(t + nwv < t1 ? t + nwv : t);
-        uint32_t ent = fsm_rec_ent(rc);
-        int32_t cnt = (int32_t)fsm_rec_cnt(rc);
-        if (fsm_fx_ok(fx)) {
-            ent = fsm_fx_ent(fx);
-            cnt += fsm_fx_d(fx);
+        for (uint32_t c = 0; c < NCH; c++) {
+            uint64_t tt = tt0 + c * nwv;
+            tt = uni64(tt < t1 ? tt : tt0);
+            const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
+            prec[c] = wk.rec[tt * NR + j];
+            pfx[c] = wk.fx[tt * FX_W + (j & (FX_W - 1))];
+            const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / SCAN_TB);
+            const uint32_t ln = j & 3u;
+            pmeta[c] = *(ln == 0 ? blk32 : ln == 1 ? blk32 + 1 : (const uint32_t *)&wk.lex[tt]);
+            fs_load<SW>(pw[c], rs, j * SW);
         }
-        const uint32_t c = (uint32_t)cnt;
-        const int32_t incl = wave_incl_scan((int32_t)c);
-        const uint32_t L = (uint32_t)incl - c;
-        const uint32_t Tout = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-        const uint64_t P0 = (uint64_t)((int64_t)(((uint64_t)bhi << 32) | blo) + lx);
-        const bool inside = P0 <= cap && Tout <= cap - P0;
-        if (j == 0 && !inside) atomicOr(wk.flags, (uint32_t)FF_OVER);
-        if (!inside) continue;
-        const uint64_t R = t * TB + (uint64_t)j * S;
-        uint32_t lim = S;
-        bool at_end = R + S == geo.bits;
-        if (TAIL) {
-            lim = R >= geo.bits ? 0u : (geo.bits - R < S ? (uint32_t)(geo.bits - R) : S);
-            at_end = R < geo.bits && R + S >= geo.bits;
-        }
-        const uint32_t a0 = (uint32_t)(P0 & 15u);
-        if (a0 + Tout + 8 <= OBW) {
-            const uint32_t oa = stage + a0 + L;
-            uint32_t fw = 0, lw = 0, lwd = 0;
-            bool fok = true;
-            WAVE_SYNC();                              // the previous tile's copy-out has read the staging
-            emf_region<SW, K, TAIL>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, &fw, &fok, &lw, &lwd);
-            WAVE_SYNC();
-            emf_edges<SW, K>(smem, s_b1, s_ts, w, ent, lim, at_end, c, oa, fw, fok, lw, lwd);
-            WAVE_SYNC();
-            // copy-out: whole 16-B blocks; the bytes of the partial first and
-            // last blocks one per lane (lanes 0..15, 16..31)
-            uint8_t *gb = out + (P0 - a0);
-            const uint8_t *sb = smem + stage;
-            const uint32_t end = a0 + Tout, nq = (end + 15u) / 16u;
-            for (uint32_t i = j; i < nq; i += 64) {
-                const uint32_t lo = 16 * i;
-                if (lo >= a0 && lo + 16 <= end)
-                    __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
+    };
+    uint64_t t = t0 + (uint64_t)blockIdx.x * nact + wv;
+    if (t < t1) prefetch(t);
+    for (; t < t1; t += NCH * nwv) {
+        uint32_t w[NCH][SW], ent[NCH], c[NCH], L[NCH], Tout[NCH], a0[NCH], oa[NCH], lim = S;
+        uint64_t P0[NCH];
+        bool at_end[NCH], fit[NCH], live[NCH];
+#pragma unroll
+        for (uint32_t x = 0; x < NCH; x++) {
+#pragma unroll
+            for (uint32_t k = 0; k < SW; k++) w[x][k] = pw[x][k];
+            const uint64_t tx = t + x * nwv;
+            live[x] = tx < t1;
+            const uint32_t rc = prec[x], fx = j < FX_W ? pfx[x] : 0u;
+            const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)pmeta[x], 0);
+            const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)pmeta[x], 1);
+            const int32_t lx = __builtin_amdgcn_readlane((int)pmeta[x], 2);
+            ent[x] = fsm_rec_ent(rc);
+            int32_t cn = (int32_t)fsm_rec_cnt(rc);
+            if (fsm_fx_ok(fx)) {
+                ent[x] = fsm_fx_ent(fx);
+                cn += fsm_fx_d(fx);
             }
-            const bool part0 = a0 != 0 || end < 16, partl = (end & 15u) != 0 && end > 16;
-            const uint32_t q = j < 16 ? j : (end & ~15u) + (j - 16);
-            if (j < 32 && (j < 16 ? part0 : partl) && q >= a0 && q < end) gb[q] = sb[q];
-        } else {
-            emf_direct<SW>(s_b1, s_ts, w, ent, lim, at_end, out + P0 + L);
+            c[x] = live[x] ? (uint32_t)cn : 0u;
+            const int32_t incl = wave_incl_scan((int32_t)c[x]);
+            L[x] = (uint32_t)incl - c[x];
+            Tout[x] = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+            P0[x] = (uint64_t)((int64_t)(((uint64_t)bhi << 32) | blo) + lx);
+            const bool inside = P0[x] <= cap && Tout[x] <= cap - P0[x];
+            if (live[x] && j == 0 && !inside) atomicOr(wk.flags, (uint32_t)FF_OVER);
+            live[x] = live[x] && inside;
+            const uint64_t R = tx * TB + (uint64_t)j * S;
+            at_end[x] = R + S == geo.bits;
+            if (TAIL) {
+                lim = R >= geo.bits ? 0u : (geo.bits - R < S ? (uint32_t)(geo.bits - R) : S);
+                at_end[x] = R < geo.bits && R + S >= geo.bits;
+            }
+            a0[x] = (uint32_t)(P0[x] & 15u);
+            fit[x] = a0[x] + Tout[x] + 8 <= obw;
+            // (a chain that does not write its staging still runs: its lanes
+            // all store at the slot's start, inside the slot)
+            oa[x] = tabb + (wv * NCH + x) * obw + (live[x] && fit[x] ? a0[x] + L[x] : 0u);
+        }
+        prefetch(t + NCH * nwv < t1 ? t + NCH * nwv : t);
+        uint32_t fw[NCH], lw[NCH], lwd[NCH];
+        bool fok[NCH];
+        WAVE_SYNC();                                  // the previous tiles' copy-out has read the staging
+        emf_region<SW, K, TAIL, NCH>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, fw, fok, lw, lwd);
+        WAVE_SYNC();
+#pragma unroll
+        for (uint32_t x = 0; x < NCH; x++)
+            if (live[x] && fit[x]) emf_edges<SW, K>(smem, s_b1, s_ts, w[x], ent[x], lim, at_end[x], c[x], oa[x], fw[x], fok[x], lw[x], lwd[x]);
+        WAVE_SYNC();
+#pragma unroll
+        for (uint32_t x = 0; x < NCH; x++) {
+            if (!live[x]) continue;
+            if (fit[x]) {
+                // copy-out: whole 16-B blocks; the bytes of the partial first
+                // and last blocks one per lane (lanes 0..15, 16..31)
+                uint8_t *gb = out + (P0[x] - a0[x]);
+                const uint8_t *sb = smem + tabb + (wv * NCH + x) * obw;
+                const uint32_t end = a0[x] + Tout[x], nq = (end + 15u) / 16u;
+                for (uint32_t i = j; i < nq; i += 64) {
+                    const uint32_t lo = 16 * i;
+                    if (lo >= a0[x] && lo + 16 <= end)
+                        __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
+                }
+                const bool part0 = a0[x] != 0 || end < 16, partl = (end & 15u) != 0 && end > 16;
+                const uint32_t q = j < 16 ? j : (end & ~15u) + (j - 16);
+                if (j < 32 && (j < 16 ? part0 : partl) && q >= a0[x] && q < end) gb[q] = sb[q];
+            } else {
+                emf_direct<SW>(s_b1, s_ts, w[x], ent[x], lim, at_end[x], out + P0[x] + L[x]);
+            }
         }
     }
 }
@@ -677,7 +827,7 @@ __global__ __launch_bounds__(64 * emf_waves(K)) void k_emf(const uint32_t *__res
 // Host side
 // ---------------------------------------------------------------------------
 typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint64_t);
-typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t);
+typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t, uint32_t);
 
 #define FSM_SW_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
 static kcnt_t kcnt_for(uint32_t sw, bool tail) {
@@ -688,27 +838,38 @@ static kcnt_t kcnt_for(uint32_t sw, bool tail) {
     default: return nullptr;
     }
 }
-static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail) {
+// chains per lane of the main emission launch (HH_EMF_NCH: experiments)
+#ifndef HH_EMF_NCH
+#define HH_EMF_NCH 1
+#endif
+static uint32_t emf_nch() {
+    const char *e = getenv("HH_EMF_NCH");
+    const uint32_t v = e ? (uint32_t)atoi(e) : HH_EMF_NCH;
+    return v == 1 ? 1u : 2u;
+}
+static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch) {
     switch (sw) {
+#define EMF_K(n, k)                                                                      \
+    (tail ? k_emf<n, k, true, 1> : nch == 2 ? k_emf<n, k, false, 2> : k_emf<n, k, false, 1>)
 #define X(n)                                                                            \
     case n:                                                                             \
-        return K == 7   ? (tail ? k_emf<n, 7, true> : k_emf<n, 7, false>)               \
-               : K == 6 ? (tail ? k_emf<n, 6, true> : k_emf<n, 6, false>)               \
-               : K == 4 ? (tail ? k_emf<n, 4, true> : k_emf<n, 4, false>) : nullptr;
+        return K == 7 ? EMF_K(n, 7) : K == 6 ? EMF_K(n, 6) : K == 4 ? EMF_K(n, 4) : nullptr;
         FSM_SW_CASES(X)
 #undef X
+#undef EMF_K
     default: return nullptr;
     }
 }
 
 static size_t lds_cnt(const FsmDev *fd) { return cnt_tab_bytes(fd->ns); }
-static size_t lds_emf(const FsmDev *fd) {
-    return emf_tab_bytes(fd->ns, fd->K, fd->r) + (size_t)emf_waves(fd->K) * emf_obw(fd->K);
-}
+// k_emf takes the whole LDS (one workgroup per CU) and sizes its stagings
+// from the largest tile output at run time
+#define EMF_LDS (160u * 1024u)
+static size_t lds_emf(const FsmDev *) { return EMF_LDS; }
 
-// 7-bit emission steps when their tables leave the staging room
+// 7-bit emission steps when their tables leave room for 16 stagings of 4 KiB
 bool fsm_k_fits(const hh_fsm_tables *F) {
-    return F->K == 7 && emf_tab_bytes(F->ns, 7, F->r) + emf_waves(7) * emf_obw(7) <= 160u * 1024u;
+    return F->K == 7 && emf_tab_bytes(F->ns, 7, F->r) + 16u * 4096u <= EMF_LDS;
 }
 
 void fsm_free(FsmDev *fd) {
@@ -724,7 +885,7 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G) {
     fsm_free(fd);
     const uint32_t ns = F->ns;
     const uint32_t sw = F->S / 32;
-    if (F->S % 32 || sw < 2 || sw > 12 || G % 8 || G > 64 || G > F->S) return HH_ERR_UNSUPPORTED;
+    if (F->S % 32 || sw < 2 || sw > 12 || G % 8 || G > HH_FSM_GMAX || G > F->S) return HH_ERR_UNSUPPORTED;
     fd->ns = ns;
     fd->K = F->K;
     fd->r = F->r;
@@ -749,12 +910,12 @@ static int fsm_grids(FsmDev *fd) {
     if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns && fd->sized_K == fd->K) return HH_OK;
     const uint32_t sw = fd->S / 32;
     const kcnt_t kc = kcnt_for(sw, false);
-    const kemf_t ke = kemf_for(sw, fd->K, false);
+    const kemf_t ke = kemf_for(sw, fd->K, false, emf_nch());
     if (!kc || !ke) return HH_ERR_UNSUPPORTED;
     int pc = 0, pe = 0, ncu = 0, dev = 0;
     FS_OK(hipGetDevice(&dev));
     FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kc, 64 * CW, lds_cnt(fd)));
-    FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, ke, 64 * emf_waves(fd->K), lds_emf(fd)));
+    FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, ke, 64 * emf_waves(emf_nch()), lds_emf(fd)));
     FS_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (pc < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
     fd->grid_c = (uint32_t)(pc * ncu);
@@ -800,7 +961,8 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     // workspace: flags 64 B | rec | tsum | xs | fx | lex | blk
     const size_t o_rec = 64, o_tsum = o_rec + nt * NR * 4, o_xs = o_tsum + nt * 4, o_fx = o_xs + nt * 4;
     const size_t o_lex = o_fx + (nt + 1) * FX_W * 4, o_blk = (o_lex + (nt + 1) * 4 + 7) & ~(size_t)7;
-    rc = ws_need(ws, o_blk + (size_t)nblk * 8);
+    const size_t o_bmax = o_blk + (size_t)nblk * 8;
+    rc = ws_need(ws, o_bmax + (size_t)nblk * 4);
     if (rc) return rc;
     uint8_t *w = (uint8_t *)ws->p;
     FsmWork wk;
@@ -811,9 +973,14 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     wk.fx = (uint32_t *)(w + o_fx);
     wk.lex = (int32_t *)(w + o_lex);
     wk.blk = (int64_t *)(w + o_blk);
+    wk.bmax = (int32_t *)(w + o_bmax);
+    wk.dbg = fd->dbg;
     FsmTab tab = {fd->ct, fd->b1, fd->tsym, fd->et, fd->er};
     const uint32_t sw = fd->S / 32;
     FS_OK(hipMemsetAsync(wk.flags, 0, 64, st));
+#ifdef HH_DIAG
+    if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, 16 * sizeof(uint64_t), st));
+#endif
     FS_OK(hipEventRecord(ev[0], st));
     {
         // tiles [0, nc) whose regions and next region end before the stream,
@@ -840,19 +1007,21 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     FS_OK(hipGetLastError());
     FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
-        const uint32_t ew = emf_waves(fd->K);
+        const uint32_t ew = emf_waves(emf_nch()), ew1 = emf_waves(1);
         // tiles that end before the stream, then the last one(s) (TAIL)
         const uint64_t ne = std::max<uint64_t>(emit_from, std::min<uint64_t>(bits / TB, nt));
         if (ne > emit_from) {
             const uint64_t nwg = (ne - emit_from + ew - 1) / ew;
             const uint32_t ge = (uint32_t)(nwg < fd->grid_e ? nwg : fd->grid_e);
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, false), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
-                               (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne);
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch()), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
+                               (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne,
+                               (uint32_t)lds_emf(fd));
             FS_OK(hipGetLastError());
         }
         if (ne < nt) {
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, true), dim3((unsigned)((nt - ne + ew - 1) / ew)), dim3(64 * ew),
-                               lds_emf(fd), st, (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt);
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, true, 1), dim3((unsigned)((nt - ne + ew1 - 1) / ew1)), dim3(64 * ew1),
+                               lds_emf(fd), st, (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt,
+                               (uint32_t)lds_emf(fd));
             FS_OK(hipGetLastError());
         }
     }

@@ -51,19 +51,25 @@
 #endif
 
 #define HH_FSM_KM 8           /* regions a late meeting may be followed into */
+#ifndef HH_FSM_GMAX
+#define HH_FSM_GMAX 128       /* longest head (bits) */
+#endif
 
 /* Head bits G (the guess of a region's entering state starts at the root G
  * bits before it): whole bytes, on the code-length lattice (a multiple of
  * the gcd of the code lengths: a chain started off it never meets the true
- * one), at most 64; none for a fixed-length code (regions start on its
- * lattice, where the root is always right). */
-HH_FD uint32_t hh_fsm_pick_head(const hh_tables *t) {
+ * one), at most HH_FSM_GMAX and the region bits S; none for a fixed-length code (regions start
+ * on its lattice, where the root is always right).  On kjv a 64-bit head
+ * leaves 6.7 % of the guesses wrong, a 128-bit head 0.3 %: a wave walks
+ * only in 15 % of its tiles. */
+HH_FD uint32_t hh_fsm_pick_head(const hh_tables *t, uint32_t S) {
     if (t->fixed_len > 0) return 0u;
     const uint32_t g = t->len_gcd > 0 ? (uint32_t)t->len_gcd : 1u;
     uint32_t a = 8, b = g;
     while (b) { const uint32_t x = a % b; a = b; b = x; }
     const uint32_t l = 8 / a * g;                  /* lcm(8, g) */
-    return l > 64 ? 0u : 64u / l * l;
+    const uint32_t gmax = S < HH_FSM_GMAX ? S : HH_FSM_GMAX;   /* (within the region before) */
+    return l > gmax ? 0u : gmax / l * l;
 }
 
 typedef struct {

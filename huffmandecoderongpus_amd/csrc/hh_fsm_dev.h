@@ -20,6 +20,7 @@ struct FsmDev {
     uint64_t *et, *er;
     // persistent grids (workgroups), sized by the occupancy API for S / ns
     uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K;
+    uint64_t *dbg;           // HH_DIAG builds: phase cycles of k_cnt (16 x u64, the decoder's)
 };
 
 // One decode of tiles [0, ntiles) of the segment at d_data (bits readable

@@ -48,8 +48,8 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
     if (S < 32 || S % 32) return HH_ERR_ARG;
     rc = hh_fsm_build(&g_T, S, g_K, &g_F);
     if (rc) return rc;
-    uint32_t G = G_req >= 0 ? (uint32_t)G_req : hh_fsm_pick_head(&g_T);
-    if (G % 8 || G > 64 || G > S) return HH_ERR_ARG;
+    uint32_t G = G_req >= 0 ? (uint32_t)G_req : hh_fsm_pick_head(&g_T, S);
+    if (G % 8 || G > HH_FSM_GMAX || G > S) return HH_ERR_ARG;
     stats[3] = S;
     stats[4] = G;
     if (leave) *leave = in_state;
@@ -212,7 +212,7 @@ int64_t hh_fsm_emu_tables(const int32_t *izero, const int32_t *ione, const uint8
     info[0] = g_F.ns;
     info[1] = g_F.K;
     info[2] = g_F.r;
-    info[3] = hh_fsm_pick_head(&g_T);
+    info[3] = hh_fsm_pick_head(&g_T, S);
     return HH_OK;
 }
 

@@ -331,11 +331,11 @@ def test_fsm_tables_shape(femu):
     sy = np.ascontiguousarray(hf.sym, np.uint8)
     assert femu.hh_fsm_emu_tables(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), 256,
                                   info.ctypes.data) == 0
-    assert list(info) == [83, 6, 4, 64]
+    assert list(info) == [83, 6, 4, 128]
     femu.hh_fsm_emu_set_k(7)
     try:
         assert femu.hh_fsm_emu_tables(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), 256,
                                       info.ctypes.data) == 0
     finally:
         femu.hh_fsm_emu_set_k(0)
-    assert list(info) == [83, 7, 4, 64]
+    assert list(info) == [83, 7, 4, 128]

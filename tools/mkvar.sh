@@ -1,0 +1,14 @@
+# Build a variant of libhiphuff.so with extra compile flags for same-box A/B
+# (tools/gpu_walkab.sh): bash tools/mkvar.sh NAME "-DFOO=1 ..." -> build/var/NAME.so
+set -e
+cd "$(dirname "$0")/.."
+N=$1; shift
+D=build/var/$N
+mkdir -p $D
+F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -Wno-comment -Iinclude -Ihuffmandecoderongpus_amd/csrc $*"
+/opt/rocm/bin/hipcc $F -c huffmandecoderongpus_amd/csrc/hh_device.hip -o $D/hh_device.o &
+/opt/rocm/bin/hipcc $F -c huffmandecoderongpus_amd/csrc/hh_fsm.hip -o $D/hh_fsm.o &
+wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o build/var/$N.so $D/hh_device.o $D/hh_fsm.o build/hh_huff.o build/hh_plugin.o
+rm -rf $D
+echo build/var/$N.so

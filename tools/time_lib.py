@@ -59,7 +59,19 @@ res = {"lib": os.path.basename(os.environ.get("HIPHUFF_LIB", H.LIB_PATH)), "mib"
        "ok": bool(ok), "fast": dec.stats()["exact_fallback"] == 0}
 res.update({k: round(statistics.median(v), 4) for k, v in ph.items()})
 res["wall_ms"] = round(statistics.median(wall[1:]), 3)
-if os.environ.get("HH_DIAG"):            # a -DHH_DIAG build: phase cycles and walk lengths
+if os.environ.get("HH_DIAG") == "fsm":     # a -DHH_DIAG build: k_cnt phase cycles and walks
+    import ctypes as C
+    buf = (C.c_uint64 * 16)()
+    H.lib().hh_debug_counters(dec._h, buf)
+    cyc = [buf[i] for i in range(4)]
+    tot = sum(cyc) or 1
+    res["cnt_phase_frac"] = {n: round(cyc[i] / tot, 3) for n, i in
+                             (("head", 0), ("count", 1), ("walks", 2), ("records", 3))}
+    res["cnt_tiles"] = buf[8]
+    res["cnt_walk_tiles"] = buf[9]
+    res["cnt_walk_rounds"] = buf[10]
+    res["cnt_cycles_per_tile"] = round(tot / max(buf[8], 1), 1)
+elif os.environ.get("HH_DIAG"):            # a -DHH_DIAG build: phase cycles and walk lengths
     import ctypes as C
     buf = (C.c_uint64 * 16)()
     H.lib().hh_debug_counters(dec._h, buf)
