@@ -5,10 +5,11 @@ Workload (BASELINE.json configs[2]): a synthetic 1 GiB English-text .huff --
 kjv.txt tiled (about 349.4 copies) and encoded with the files/kjv.txt.huff
 codebook, cut at a symbol boundary -- decoded on each MI355X.  One "step" is
 one full decode of that stream with the input already resident in HBM:
-hh_decode_device (k_front: overlap heads, speculative region decode, exit
-merges; k_walk: the deferred walks; k_table: transfer tables;
-k_scan1/k_scan2: entering states and tile bases; k_emit + k_emitx:
-emission) plus its status readback.  For N > 1 the stream is N GiB, sharded
+hh_decode_device -- the state-machine decode (k_cnt: 128-bit heads, each
+region's count and exit state in 8-bit steps of the count table, walks
+where a guessed entering state was wrong; k_fscan1/k_fscan2: tile bases;
+k_emf: emission in 7-bit steps into LDS staging, 16-B copy-out) -- plus its
+status readback.  For N > 1 the stream is N GiB, sharded
 by whole tiles (weak scaling); each step is the rank's segment decode (with
 its prologue tiles) plus the entry-state exchange (one 5-integer
 all-gather); the decoded segments are all-gathered once after the timed
@@ -58,12 +59,12 @@ def _args():
     return ap.parse_args()
 
 
-def cpu_baseline(files_dir: str, seconds: float) -> dict:
-    """linApproach on kjv.txt.huff, one core: sweep jumpbits 1..14 once
+def cpu_baseline(files_dir: str, seconds: float, name: str = "kjv.txt.huff") -> dict:
+    """linApproach on files/<name>, one core: sweep jumpbits 1..14 once
     (the reference's testall sweep, mainrun.c:456-459), then repeat the best
     for ~`seconds`; report decoded MB/s of the median repeat."""
     from oracle import oracle as O
-    path = os.path.join(files_dir, "kjv.txt.huff")
+    path = os.path.join(files_dir, name)
     if O.ref_available():
         kind = "reference"
         h = O.RefHuff(path)
@@ -98,7 +99,7 @@ def cpu_baseline(files_dir: str, seconds: float) -> dict:
     except OSError:
         pass
     return {"value": round(D / med / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": kind,
-            "sample": (f"linApproach(jumpbits={best_j}) on files/kjv.txt.huff "
+            "sample": (f"linApproach(jumpbits={best_j}) on files/{name} "
                        f"({D} B decoded), median of {len(times)} runs over ~{seconds:.0f} s, "
                        f"tables built inside each timed call; host {cpu}, "
                        f"nproc {os.cpu_count()}")}
@@ -162,6 +163,28 @@ def evaluate_scope(H, hf, payload, bits: int, n_want: int, reps: int, check=None
                 "MBps": round(n_want / (ms * 1e-3) / 1e6, 1), "decoded_bytes": n_want, "reps": reps}
     finally:
         dec.close()
+
+
+def copy_rate(dev, nbytes: int, reps: int = 5) -> dict:
+    """Device-to-device copy of `nbytes` on the same GPU (torch copy_,
+    read + write = 2 x nbytes moved): the HBM rate a streaming kernel
+    reaches on this box, the reference for `frac_vs_copy`."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(reps):
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    del a, b
+    torch.cuda.empty_cache()
+    ms = statistics.median(ts)
+    return {"GBps": round(2 * nbytes / (ms * 1e-3) / 1e9, 1), "bytes_moved": 2 * nbytes, "ms": round(ms, 4)}
 
 
 def load_pmc(path: str, workload: str):
@@ -280,6 +303,8 @@ def main():
     phases = {k: round(statistics.mean(s[f"ms_{k}"] for s in dev_ms), 4)
               for k in ("sync", "scan", "emit")}
     fast = all(s["exact_fallback"] == 0 for s in dev_ms)
+    kernels = ("k_cnt+k_fscan1+k_fscan2+k_emf" if all(s["state_machine"] for s in dev_ms)
+               else "k_front+k_walk+k_table+k_scan1+k_scan2+k_emit")
     extra = {}
     if world > 1:
         extra = job.gather_report()
@@ -308,7 +333,7 @@ def main():
         "config": {"workload": workload + (f", sharded over {world} GPUs" if world > 1 else ", 1 MI355X"),
                    "compressed_bytes": C_all, "decoded_bytes": D_all,
                    "bits_per_gpu": int(C_bytes * 8), "parallelism": f"byte-range shards x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_front+k_walk+k_table+k_scan1+k_scan2+k_emit",
+        "roofline": {"bound": "hbm", "kernel": kernels,
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_alg": C_bytes + D_bytes, "ms_kernel": round(ms_dev, 4),
@@ -318,6 +343,11 @@ def main():
         "fast_path": fast,
     }
     res.update(extra)
+    if world == 1:
+        # the same box's streaming rate over the same bytes (after the timed region)
+        cp = copy_rate(dev, (C_bytes + D_bytes) // 2)
+        res["roofline"]["copy_GBps"] = cp["GBps"]
+        res["roofline"]["frac_vs_copy"] = round(achieved / cp["GBps"], 4)
     if world == 1 and not a.no_extra:
         # SURVEY 8d's other single-GPU configs and the evaluate() scope
         # (after the headline measurement, outside its timed region)
@@ -366,6 +396,9 @@ def main():
         res["evaluate"] = ev
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.files, a.cpu_seconds)
+        if "workloads" in res:
+            # beside the E.coli workload: the reference's best jumpbits differs there
+            res["workloads"][0]["cpu_baseline"] = cpu_baseline(a.files, a.cpu_seconds, "E.coli.huff")
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -213,6 +213,13 @@ __device__ __forceinline__ uint32_t b1_row(const uint32_t *b1, uint32_t row, uin
     return (v & 255u) << 9;
 }
 
+// The rare cross-tile fixer out of line: its registers do not add to the
+// count loop's peak (the caller's live values are saved around the call)
+__device__ __noinline__ int cnt_fix_next(const hh_fsm_view *F, const uint32_t *w, uint64_t T1, uint32_t S,
+                                         uint64_t bits, uint32_t x, uint32_t h, uint32_t *fx) {
+    return fsm_fix_next(F, w, T1, S, bits, x, h, fx);
+}
+
 // ---------------------------------------------------------------------------
 // Region passes of k_cnt on words in registers (states as rows).  lim: the
 // region's readable bits (S unless the stream ends inside it); only the TAIL
@@ -294,7 +301,7 @@ __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns) {
 template <uint32_t SW, bool TAIL>
 __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
                                          const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
-                                         const uint32_t *nx CDIAG_ARGS) {
+                                         const uint32_t *nx, const uint32_t *pv CDIAG_ARGS) {
     constexpr uint32_t S = 32 * SW;
     const uint32_t j = threadIdx.x & 63u;
     const uint64_t TB = (uint64_t)NR * S, T0 = t * TB;
@@ -309,21 +316,31 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
 
     // decodeallbits: the guess for region j+1 (a chain started at the root G
     // bits before it), then region j from the guess lane j-1 made for it
-    uint32_t gs = 0;
+    uint32_t gs = 0, hp = 0;
 #ifndef HH_XP_NOHEAD
 #define HH_XP_NOHEAD 0        // (timing experiments only: results are wrong)
 #endif
     if (geo.G && !HH_XP_NOHEAD) {
+        // and lane 0's guess for its own region 0 (tile t > 0): the same head
+        // over the previous region's last G bits -- uniform words (scalar
+        // loads), a chain every lane runs alike (broadcast reads), interleaved
+        // with its own head
         const uint32_t GB = geo.G >> 3;                   // (uniform)
         constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
+        static_assert(HB % 4 == 0, "head bytes in whole words");
 #pragma unroll
         for (uint32_t k = 4 * SW - HB; k < 4 * SW; k++)
-            if (k >= 4 * SW - GB) gs = ct_at(lds, gs, rbyte<SW>(w, k));
+            if (k >= 4 * SW - GB) {
+                const uint32_t q = k - (4 * SW - HB);
+                gs = ct_at(lds, gs, rbyte<SW>(w, k));
+                hp = ct_at(lds, hp, __builtin_amdgcn_ubfe(pv[q >> 2], 8 * (q & 3), 8));
+            }
         gs &= 0xfe00u;
+        hp &= 0xfe00u;
     }
     CDIAG_STAMP(0);
     const uint32_t gup = shfl_up1(gs);              // (cross-lane ops with every lane active)
-    const uint32_t sp = j ? gup : (t == 0 ? geo.in_state << 9 : 0u);
+    const uint32_t sp = j ? gup : (t == 0 ? geo.in_state << 9 : hp);
     uint32_t n;
     uint32_t X = cnt_region<SW, TAIL>(lds, F.b1, w, sp, lim, &n);   // region j's exit (given its entry)
     // the stream ends in region j / in region j+1: the tail rule counts a
@@ -339,7 +356,7 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     // becomes the exit.  A walk that does not meet in its region changes that
     // region's exit: the next lane walks again in the next round.  The
     // corrections telescope: d = count(true chain) - count(first assumption).
-    uint32_t E = j == 63 ? 0u : gs;
+    uint32_t E = gs;                                // (lane 63: the next tile's region 0, guessed alike)
     int32_t d = 0;
     bool lost = false;                              // lane 63: not met in the next tile's region 0
 #ifndef HH_XP_NOWALK
@@ -387,29 +404,43 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     const uint32_t Eup = shfl_up1(E), dup = shfl_up1((uint32_t)d);
     const uint32_t ent = (j ? Eup : sp) >> 9;
     const uint32_t cnt = (uint32_t)((int32_t)n + (j ? (int32_t)dup : 0));
+    // the tile's stores are unconditional (every lane the same value where a
+    // word is the tile's: one store instruction, no branch), so that the
+    // compiler can count them and the next tile waits only for its prefetched
+    // words, not for these stores to reach memory
     wk.rec[t * NR + j] = fsm_rec(ent, cnt);
     const int32_t sum = wave_sum((int32_t)cnt);
     const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63) >> 9;
-    if (j == 0) {
-        wk.tsum[t] = sum;
-        wk.xs[t] = x;
-    }
-    // the next tile's corrections (its region 0 assumed entered at the root)
-    if (t == 0 && j < FX_W) wk.fx[j] = 0u;
+    wk.tsum[t] = sum;
+    // the next tile's corrections (its region 0 assumed entered in the head
+    // guess, lane 63's gs); lanes j and j + 8k store the same word
+    uint32_t fxv = 0, fail = 0;
     if (has_next) {
         const bool lst = __builtin_amdgcn_readlane((int)lost, 63) != 0;
         if (!lst) {
             const uint32_t E63 = (uint32_t)__builtin_amdgcn_readlane((int)E, 63) >> 9;
             const int32_t d63 = __builtin_amdgcn_readlane(d, 63);
-            if (j < FX_W) wk.fx[(t + 1) * FX_W + j] = j == 0 && (E63 | (uint32_t)d63) ? fsm_fx(E63, d63) : 0u;
-        } else if (j == 0) {
-            // rare: the chains meet beyond the next tile's region 0 (words
-            // from global memory)
-            uint32_t f[FX_W];
-            if (!fsm_fix_next(&F, g, T0 + TB, S, geo.bits, x, f)) atomicOr(wk.flags, (uint32_t)FF_FAIL);
-            for (int i = 0; i < FX_W; i++) wk.fx[(t + 1) * FX_W + i] = f[i];
+            const uint32_t g63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> 9;
+            const bool walked = E63 != g63 || d63 != 0;      // (lane 63 walked into the next tile)
+            fxv = (j & (FX_W - 1)) == 0 && walked ? fsm_fx(E63, d63) : 0u;
+        } else {
+            // rare: the chains meet beyond the next tile's region 0 (lane 0,
+            // words from global memory)
+            uint32_t f[FX_W], ok = 1;
+            const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> 9;
+            if (j == 0) ok = cnt_fix_next(&F, g, T0 + TB, S, geo.bits, x, h63, f);
+            else
+                for (int i = 0; i < FX_W; i++) f[i] = 0;
+#pragma unroll
+            for (int i = 0; i < FX_W; i++) {
+                const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)f[i], 0);
+                fxv = (j & (FX_W - 1)) == (uint32_t)i ? v : fxv;
+            }
+            fail = __builtin_amdgcn_readlane((int)ok, 0) ? 0u : 1u;
         }
     }
+    wk.fx[(t + 1) * FX_W + (j & (FX_W - 1))] = fxv;   // ((ntiles + 1) x FX_W words: the last tile's too)
+    wk.xs[t] = x | fail << 31;                        // (bit 31: chains that did not meet, k_fscan reports it)
     CDIAG_STAMP(3);
 }
 
@@ -430,30 +461,46 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
     __syncthreads();
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts};
-    const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * CW;
-    uint64_t t = t0 + (uint64_t)blockIdx.x * CW + wv;
+    const uint64_t TB = (uint64_t)NR * S;
+    // tile indices fit 32 bits (2^32 tiles of >= 512 bytes); uniform, kept
+    // in scalar registers
+    const uint32_t nwv = gridDim.x * CW, te = (uint32_t)t1;
+    uint32_t t = (uint32_t)t0 + blockIdx.x * CW + wv;
     // the next tile's words are loaded one tile ahead: region j's and region
     // j+1's (used only by walks; waiting for them at the walk, behind the
     // previous tile's stores, cost as much as the walks themselves)
-    uint32_t pw[SW], pn[SW] = {};
-    auto prefetch = [&](uint64_t tt) {
-        tt = uni64(tt);
-        const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
-        fs_load<SW>(pw, rs, j * SW);
-        if (HH_CNT_PNX) fs_load<SW>(pn, rs, (j + 1) * SW);
+    // (and the HB bytes before the tile, for lane 0's head: lane i loads word
+    // i -- a scalar load would be waited for by every LDS wait of the tile,
+    // since scalar loads return out of order and share the LDS counter)
+    constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
+    uint32_t pw[SW], pn[SW] = {}, ppv;
+    auto prefetch = [&](uint32_t tt) {
+        tt = (uint32_t)__builtin_amdgcn_readfirstlane((int)tt);
+        const uint64_t tw = (uint64_t)tt * TB / 32, pa = tw >= HB / 4 ? tw - HB / 4 : 0u;   // (tile 0: unused)
+        const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tw, geo.nwords);
+        // (the lane id recomputed here: the register budget has no room to
+        // keep the load offsets live across the tile)
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        fs_load<SW>(pw, rs, ln * SW);
+        if (HH_CNT_PNX) fs_load<SW>(pn, rs, (ln + 1) * SW);
+        ppv = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (ln % (HB / 4))), 0, 0);
     };
     CDIAG_DECL
-    if (t < t1) prefetch(t);
-    for (; t < t1; t += nwv) {
-        uint32_t w[SW], nx[SW];
+    if (t == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
+    if (t < te) prefetch(t);
+    for (; t < te; t += nwv) {
+        t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+        uint32_t w[SW], nx[SW], pv[HB / 4];
 #pragma unroll
         for (uint32_t k = 0; k < SW; k++) {
             w[k] = pw[k];
             nx[k] = pn[k];
         }
-        if (!HH_CNT_PNX) fs_load<SW>(nx, fs_rsrc(g, uni64(t) * TB / 32, geo.nwords), (j + 1) * SW);
-        prefetch(t + nwv < t1 ? t + nwv : t);
-        cnt_tile<SW, TAIL>(smem, F, g, geo, wk, t, w, nx CDIAG_PASS);
+#pragma unroll
+        for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
+        prefetch(t + nwv < te ? t + nwv : t);
+        cnt_tile<SW, TAIL>(smem, F, g, geo, wk, (uint64_t)t, w, nx, pv CDIAG_PASS);
     }
     CDIAG_FLUSH(wk.dbg);
 }
@@ -473,6 +520,9 @@ __global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk) {
 #pragma unroll
         for (int i = 0; i < FX_W; i++) c += fsm_fx_d(wk.fx[t * FX_W + i]);
     }
+    // a tile whose last chain met no other within HH_FSM_KM regions (k_cnt
+    // marks its leaving state)
+    if (__ballot(t < geo.ntiles && (wk.xs[t] >> 31)) && (threadIdx.x & 63u) == 0) atomicOr(wk.flags, (uint32_t)FF_FAIL);
     const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
     const int32_t x = wave_incl_scan(c);
     int32_t m = c;
@@ -532,7 +582,7 @@ __global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_
         wk.flags[6] = (uint32_t)mx;       // the largest tile output (symbols)
         wk.flags[2] = (uint32_t)carry;
         wk.flags[3] = (uint32_t)((uint64_t)carry >> 32);
-        wk.flags[4] = geo.ntiles ? wk.xs[geo.ntiles - 1] : geo.in_state;
+        wk.flags[4] = geo.ntiles ? wk.xs[geo.ntiles - 1] & 255u : geo.in_state;
         uint32_t en = geo.in_state;
         if (geo.emit_from < geo.ntiles) {
             const uint32_t f = wk.fx[geo.emit_from * FX_W];

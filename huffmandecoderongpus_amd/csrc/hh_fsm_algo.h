@@ -193,15 +193,16 @@ HH_FD uint32_t fsm_fx_ent(uint32_t f) { return (f >> 1) & 255u; }
 HH_FD int32_t fsm_fx_d(uint32_t f) { return (int32_t)f >> 16; }
 
 /* The chain leaving tile t in state x (its true exit) against tile t+1's
- * assumption (entered at the root, each region's recorded entering state
- * the one its predecessor left it in): followed region by region from tile
- * t+1's start until they meet.  fx[r] (r < HH_FSM_KM) receives the
- * corrections of tile t+1's regions; returns 0 if they did not meet within
- * HH_FSM_KM regions.  T1 = tile t+1's first bit, S region bits. */
+ * assumption (region 0 entered in state h -- the head guess, from the root G
+ * bits before the tile -- each later region in the state its predecessor
+ * left it in): followed region by region from tile t+1's start until they
+ * meet.  fx[r] (r < HH_FSM_KM) receives the corrections of tile t+1's
+ * regions; returns 0 if they did not meet within HH_FSM_KM regions.  T1 =
+ * tile t+1's first bit, S region bits. */
 HH_FD int fsm_fix_next(const hh_fsm_view *F, const uint32_t *w, uint64_t T1, uint32_t S, uint64_t bits,
-                       uint32_t x, uint32_t *fx) {
+                       uint32_t x, uint32_t h, uint32_t *fx) {
     for (int r = 0; r < HH_FSM_KM; r++) fx[r] = 0;
-    uint32_t a = x, b = 0;
+    uint32_t a = x, b = h;
     for (int r = 0; r < HH_FSM_KM; r++) {
         const uint64_t R = T1 + (uint64_t)r * S;
         if (a == b || R >= bits) return 1;   /* met, or past the end: nothing more to correct */

@@ -76,8 +76,15 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
             g[j] = 0;
             if (G && R1 - G < bits) g[j] = fsm_run(&F, w, R1 - G, R1 < bits ? R1 : bits, 0u, &c);
         }
+        // region 0 of a later tile: the head guess from the G bits before it
+        // (the same chain the previous tile's last lane computed as g[NR-1])
+        uint32_t h0 = 0;
+        if (t > 0 && G) {
+            uint32_t c = 0;
+            h0 = fsm_run(&F, w, T0 - G, T0, 0u, &c);
+        }
         for (int j = 0; j < NR; j++) {
-            sp[j] = j ? g[j - 1] : (t == 0 ? in_state : 0u);
+            sp[j] = j ? g[j - 1] : (t == 0 ? in_state : h0);
             const uint64_t R = T0 + (uint64_t)j * S;
             tx[j] = fsm_region(&F, w, R, R + S, bits, sp[j], &n[j]);
         }
@@ -128,9 +135,9 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
             sum += cnt[j];
         }
         tsum[t] = sum;
-        if (t + 1 < nt && x != 0) {
+        if (t + 1 < nt && x != g[NR - 1]) {
             stats[5]++;
-            if (!fsm_fix_next(&F, w, T0 + TB, S, bits, x, &fx[(t + 1) * HH_FSM_KM])) return HH_ERR_UNSUPPORTED;
+            if (!fsm_fix_next(&F, w, T0 + TB, S, bits, x, g[NR - 1], &fx[(t + 1) * HH_FSM_KM])) return HH_ERR_UNSUPPORTED;
             stats[6] += fsm_fx_ok(fx[(t + 1) * HH_FSM_KM + 1]) != 0;
         }
         stats[0]++;

@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
+timeout -k 10 600 python3 -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t9.log 2>&1; rc=$?; echo "tests rc=$rc"; tail -4 gpurun_out/t9.log
+[ $rc -ge 124 ] && exit 1
+ROUNDS=1 bash tools/gpu_ab.sh "diag HH_DIAG=fsm" "-" "nowalk" "diag HH_DIAG=fsm HH_FSM_HEAD=64" > gpurun_out/ab9.txt 2>&1; cat gpurun_out/ab9.txt
