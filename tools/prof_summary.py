@@ -85,12 +85,29 @@ def main():
             d["wait_frac"] = round(d.get("SQ_WAIT_ANY", 0) / d["SQ_WAVE_CYCLES"], 3)
             d["active_frac"] = round(d.get("SQ_ACTIVE_INST_ANY", 0) / d["SQ_WAVE_CYCLES"], 3)
     res["hbm_bytes_per_decode"] = tot_bytes or None
+    # FETCH_SIZE calibration on known byte counts (build/ub_fetch: 1 GiB read
+    # with 16-B per-lane loads and with 4-B per-lane loads): bytes per KiB
+    # counted, for each load shape; the decoder's kernels read the payload
+    # with 16-B loads and their records with 4-B loads
+    cal = {}
+    for path in csvs(prof, "cal", "*counter_collection.csv"):
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                n = r.get("Kernel_Name", "")
+                key = "read16" if "k_read16" in n else "read4" if "k_read4" in n else None
+                if key and r["Counter_Name"] == "FETCH_SIZE":
+                    cal[key] = cal.get(key, 0.0) + float(r["Counter_Value"])
+    if cal:
+        res["fetch_calibration"] = {k: {"fetch_kib": v, "bytes_read": 1 << 30,
+                                        "bytes_per_fetch_kib": round((1 << 30) / (v * 1024.0), 3)}
+                                    for k, v in cal.items()}
     with open(os.path.join(out_dir, f"{tag}_kernels.json"), "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     if tot_bytes:
         with open(os.path.join(out_dir, "pmc_latest.json"), "w") as f:
             json.dump({"workload": workload, "tag": tag, "hbm_bytes_per_decode": tot_bytes,
-                       "per_kernel": {k: d.get("hbm_bytes") for k, d in res["kernels"].items()}},
+                       "per_kernel": {k: d.get("hbm_bytes") for k, d in res["kernels"].items()},
+                       "fetch_calibration": res.get("fetch_calibration")},
                       f, indent=1)
     print(json.dumps(res, indent=1, sort_keys=True))
 

@@ -23,4 +23,6 @@ run fetch --pmc FETCH_SIZE
 run write --pmc WRITE_SIZE
 run sq1 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU
 run sq2 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_SMEM
+# FETCH_SIZE calibration: 1 GiB read with 16-B and with 4-B per-lane loads
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $R/cal -o run -- build/ub_fetch > $R/cal.log 2>&1 || { tail -20 $R/cal.log; exit 1; }
 echo "[$(date +%T)] done"
