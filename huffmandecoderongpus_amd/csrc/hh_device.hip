@@ -1490,7 +1490,7 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
         if (d->ev[i]) hipEventDestroy(d->ev[i]);
     if (d->stream) hipStreamDestroy(d->stream);
     fsm_free(&d->fsm);
-    if (d->fsm_ws.p) hipFree(d->fsm_ws.p);
+    fsm_ws_free(&d->fsm_ws);
     for (uint32_t i = 0; i < d->npipe_ev; i++) hipEventDestroy(d->pipe_ev[i]);
     free(d->pipe_ev);
     if (d->h2d) hipStreamDestroy(d->h2d);
@@ -1580,7 +1580,7 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
         uint32_t Gf = hh_fsm_pick_head(d->ht, d->S);
         if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) & ~7u;   // experiments
         if (Gf > d->S) Gf = 0;
-        const int urc = fsm_upload(&d->fsm, d->ft, Gf);
+        const int urc = fsm_upload(&d->fsm, d->ft, Gf, (uint32_t)d->ht->minlen);
         d->fsm.dbg = d->d_dbg;
         if (urc != HH_OK && urc != HH_ERR_UNSUPPORTED) return urc;
     }

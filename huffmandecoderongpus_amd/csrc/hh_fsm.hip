@@ -49,7 +49,8 @@
 #endif
 #define CW HH_CW               // k_cnt: waves per workgroup
 #ifndef HH_CNT_PNX
-#define HH_CNT_PNX 0          // k_cnt: region j+1's words prefetched a tile ahead (1) or loaded at a walk (0)
+#define HH_CNT_PNX 0          // k_cnt walks: region j+1's words prefetched a tile ahead (1) or loaded at
+                              // a walk (0); reading them from lane j+1 measured no faster
 #endif
 #ifndef HH_WALK_MASK
 #define HH_WALK_MASK 1        // k_cnt walks: only the lanes not met yet look up
@@ -101,7 +102,13 @@ struct FsmWork {
 #define CDIAG_COUNT(i, v) do { cg_n[i] += (v); } while (0)
 #define CDIAG_FLUSH(dbg) do { if ((threadIdx.x & 63u) == 0) { for (int i_ = 0; i_ < 4; i_++) atomicAdd((unsigned long long *)&(dbg)[i_], (unsigned long long)cg_acc[i_]); \
     for (int i_ = 0; i_ < 3; i_++) atomicAdd((unsigned long long *)&(dbg)[8 + i_], (unsigned long long)cg_n[i_]); } } while (0)
+#define EDIAG_DECL uint64_t eg_acc[4] = {0, 0, 0, 0}; uint64_t eg_t = __builtin_amdgcn_s_memtime();
+#define EDIAG_STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); eg_acc[i] += t_ - eg_t; eg_t = t_; } while (0)
+#define EDIAG_FLUSH(dbg) do { if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 4; i_++) atomicAdd((unsigned long long *)&(dbg)[4 + i_], (unsigned long long)eg_acc[i_]); } while (0)
 #else
+#define EDIAG_DECL
+#define EDIAG_STAMP(i) do {} while (0)
+#define EDIAG_FLUSH(dbg) do {} while (0)
 #define CDIAG_DECL
 #define CDIAG_STAMP(i) do {} while (0)
 #define CDIAG_COUNT(i, v) do {} while (0)
@@ -371,7 +378,7 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
         uint32_t A = X, B = want ? E : X;           // (not walking: A == B, no change)
         int32_t dd = 0;
         if (round == 0) {
-            if (HH_CNT_PNX) {
+            if (HH_CNT_PNX == 1) {
 #pragma unroll
                 for (uint32_t k = 0; k < SW; k++) nv[k] = nx[k];
             } else {
@@ -547,7 +554,7 @@ __global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk) {
 }
 
 // One block: block totals -> exclusive block bases; totals and states.
-__global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_t nblk) {
+__global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_t nblk, uint32_t *res) {
     __shared__ int64_t s_w[16];
     __shared__ int32_t s_mx[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -580,15 +587,21 @@ __global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_
     if (tid == 0) {
         for (uint32_t i = 0; i < 16; i++) mx = max(mx, s_mx[i]);
         wk.flags[6] = (uint32_t)mx;       // the largest tile output (symbols)
-        wk.flags[2] = (uint32_t)carry;
-        wk.flags[3] = (uint32_t)((uint64_t)carry >> 32);
-        wk.flags[4] = geo.ntiles ? wk.xs[geo.ntiles - 1] & 255u : geo.in_state;
+        const uint32_t fl = wk.flags[0];
+        wk.flags[0] = 0u;                 // (k_fscan1's status of this decode read: cleared for the next)
+        const uint32_t lv = geo.ntiles ? wk.xs[geo.ntiles - 1] & 255u : geo.in_state;
         uint32_t en = geo.in_state;
         if (geo.emit_from < geo.ntiles) {
             const uint32_t f = wk.fx[geo.emit_from * FX_W];
             en = fsm_fx_ok(f) ? fsm_fx_ent(f) : fsm_rec_ent(wk.rec[geo.emit_from * NR]);
         }
-        wk.flags[5] = en;
+        // the host's copy (mapped memory), read after the stream's sync
+        res[0] = fl;
+        res[2] = (uint32_t)carry;
+        res[3] = (uint32_t)((uint64_t)carry >> 32);
+        res[4] = lv;
+        res[5] = en;
+        res[6] = (uint32_t)mx;
     }
 }
 
@@ -749,7 +762,15 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
 // (flags[6], k_fscan2): as many waves of the workgroup are active as the
 // LDS beside the tables holds NCH tile stagings for (up to EW), so that
 // typical streams keep more chains in flight than a worst-case size allows.
-template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH>
+// SCO: the tree bounds every tile's output by EMF_COI KiB (the host checks),
+// so the copy-out is EMF_COI unrolled lane-masked 16-B stores and no tile
+// takes the direct path: the number of stores per tile is a compile-time
+// constant, and the next tile's wait for its prefetched words (vmcnt counts
+// loads and stores in order) need not wait for this tile's stores to reach
+// memory -- with a data-dependent store loop it must (30 % of the kernel's
+// wave cycles were that wait).
+#define EMF_COI 16
+template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO>
 __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1,
                                                  uint32_t lds_bytes) {
@@ -798,6 +819,7 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
         }
     };
     uint64_t t = t0 + (uint64_t)blockIdx.x * nact + wv;
+    EDIAG_DECL
     if (t < t1) prefetch(t);
     for (; t < t1; t += NCH * nwv) {
         uint32_t w[NCH][SW], ent[NCH], c[NCH], L[NCH], Tout[NCH], a0[NCH], oa[NCH], lim = S;
@@ -825,7 +847,7 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
             Tout[x] = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
             P0[x] = (uint64_t)((int64_t)(((uint64_t)bhi << 32) | blo) + lx);
             const bool inside = P0[x] <= cap && Tout[x] <= cap - P0[x];
-            if (live[x] && j == 0 && !inside) atomicOr(wk.flags, (uint32_t)FF_OVER);
+            // (a tile past the capacity: the host reports it, total > cap)
             live[x] = live[x] && inside;
             const uint64_t R = tx * TB + (uint64_t)j * S;
             at_end[x] = R + S == geo.bits;
@@ -843,34 +865,57 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
         uint32_t fw[NCH], lw[NCH], lwd[NCH];
         bool fok[NCH];
         WAVE_SYNC();                                  // the previous tiles' copy-out has read the staging
+        EDIAG_STAMP(0);
         emf_region<SW, K, TAIL, NCH>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, fw, fok, lw, lwd);
         WAVE_SYNC();
+        EDIAG_STAMP(1);
 #pragma unroll
         for (uint32_t x = 0; x < NCH; x++)
             if (live[x] && fit[x]) emf_edges<SW, K>(smem, s_b1, s_ts, w[x], ent[x], lim, at_end[x], c[x], oa[x], fw[x], fok[x], lw[x], lwd[x]);
         WAVE_SYNC();
+        EDIAG_STAMP(2);
 #pragma unroll
         for (uint32_t x = 0; x < NCH; x++) {
-            if (!live[x]) continue;
-            if (fit[x]) {
+            if (!SCO && !live[x]) continue;      // (SCO: no branch around the stores; a dead tile's resource is empty)
+            if (SCO || fit[x]) {
                 // copy-out: whole 16-B blocks; the bytes of the partial first
                 // and last blocks one per lane (lanes 0..15, 16..31)
                 uint8_t *gb = out + (P0[x] - a0[x]);
                 const uint8_t *sb = smem + tabb + (wv * NCH + x) * obw;
                 const uint32_t end = a0[x] + Tout[x], nq = (end + 15u) / 16u;
-                for (uint32_t i = j; i < nq; i += 64) {
-                    const uint32_t lo = 16 * i;
-                    if (lo >= a0[x] && lo + 16 <= end)
-                        __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
-                }
                 const bool part0 = a0[x] != 0 || end < 16, partl = (end & 15u) != 0 && end > 16;
                 const uint32_t q = j < 16 ? j : (end & ~15u) + (j - 16);
-                if (j < 32 && (j < 16 ? part0 : partl) && q >= a0[x] && q < end) gb[q] = sb[q];
+                const bool pb = j < 32 && (j < 16 ? part0 : partl) && q >= a0[x] && q < end;
+                if (SCO) {
+                    // unconditional buffer stores: the resource spans the
+                    // tile's bytes [0, end), so the hardware drops a store
+                    // past it; lanes with nothing to store get an offset
+                    // past it too -- no branch, a fixed number of stores
+                    const __amdgpu_buffer_rsrc_t ors =
+                        __builtin_amdgcn_make_buffer_rsrc(gb, 0, (int)(live[x] ? end : 0u), 0x00020000);
+#pragma unroll
+                    for (uint32_t ii = 0; ii < EMF_COI; ii++) {
+                        const uint32_t lo = 16 * (j + 64 * ii);
+                        u32x4 v = {0u, 0u, 0u, 0u};
+                        if (lo < end) v = *(const u32x4 *)(sb + lo);   // (LDS reads only where the tile has bytes)
+                        __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(lo >= a0[x] ? lo : 0x40000000u), 0, 0);
+                    }
+                    __builtin_amdgcn_raw_buffer_store_b8(sb[q], ors, (int)(pb ? q : 0x40000000u), 0, 0);
+                } else {
+                    for (uint32_t i = j; i < nq; i += 64) {
+                        const uint32_t lo = 16 * i;
+                        if (lo >= a0[x] && lo + 16 <= end)
+                            __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
+                    }
+                    if (pb) gb[q] = sb[q];
+                }
             } else {
                 emf_direct<SW>(s_b1, s_ts, w[x], ent[x], lim, at_end[x], out + P0[x] + L[x]);
             }
         }
+        EDIAG_STAMP(3);
     }
+    EDIAG_FLUSH(wk.dbg);
 }
 
 // ---------------------------------------------------------------------------
@@ -888,19 +933,13 @@ static kcnt_t kcnt_for(uint32_t sw, bool tail) {
     default: return nullptr;
     }
 }
-// chains per lane of the main emission launch (HH_EMF_NCH: experiments)
-#ifndef HH_EMF_NCH
-#define HH_EMF_NCH 1
-#endif
-static uint32_t emf_nch() {
-    const char *e = getenv("HH_EMF_NCH");
-    const uint32_t v = e ? (uint32_t)atoi(e) : HH_EMF_NCH;
-    return v == 1 ? 1u : 2u;
-}
-static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch) {
+// chains per lane of the main emission launch
+static uint32_t emf_nch() { return 1u; }
+static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sco) {
+    (void)nch;   // (two chains per lane: measured slower, not instantiated)
     switch (sw) {
 #define EMF_K(n, k)                                                                      \
-    (tail ? k_emf<n, k, true, 1> : nch == 2 ? k_emf<n, k, false, 2> : k_emf<n, k, false, 1>)
+    (tail ? k_emf<n, k, true, 1, false> : sco ? k_emf<n, k, false, 1, true> : k_emf<n, k, false, 1, false>)
 #define X(n)                                                                            \
     case n:                                                                             \
         return K == 7 ? EMF_K(n, 7) : K == 6 ? EMF_K(n, 6) : K == 4 ? EMF_K(n, 4) : nullptr;
@@ -931,7 +970,7 @@ void fsm_free(FsmDev *fd) {
     memset(fd, 0, sizeof(*fd));
 }
 
-int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G) {
+int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen) {
     fsm_free(fd);
     const uint32_t ns = F->ns;
     const uint32_t sw = F->S / 32;
@@ -941,6 +980,11 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G) {
     fd->r = F->r;
     fd->S = F->S;
     fd->G = G;
+    // every tile's output is at most 64 S / minlen symbols (+ the tail rule's)
+    const uint64_t tmax = (uint64_t)NR * F->S / (minlen ? minlen : 1u) + 1u;
+    // (measured no faster than the store loop -- the time moved from the
+    // wait at the tile start into the stores -- so it is opt-in: HH_EMF_SCO)
+    fd->sco = tmax + 16u + 8u + 15u <= (uint64_t)EMF_COI * 1024u && getenv("HH_EMF_SCO");
     if (lds_emf(fd) > 160 * 1024 || lds_cnt(fd) > 160 * 1024) return HH_ERR_UNSUPPORTED;
     FS_OK(hipMalloc(&fd->ct, (size_t)ns * 512));
     FS_OK(hipMalloc(&fd->b1, (size_t)ns * 8));
@@ -957,10 +1001,11 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G) {
 }
 
 static int fsm_grids(FsmDev *fd) {
-    if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns && fd->sized_K == fd->K) return HH_OK;
+    if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns && fd->sized_K == fd->K && fd->sized_sco == fd->sco)
+        return HH_OK;
     const uint32_t sw = fd->S / 32;
     const kcnt_t kc = kcnt_for(sw, false);
-    const kemf_t ke = kemf_for(sw, fd->K, false, emf_nch());
+    const kemf_t ke = kemf_for(sw, fd->K, false, emf_nch(), fd->sco);
     if (!kc || !ke) return HH_ERR_UNSUPPORTED;
     int pc = 0, pe = 0, ncu = 0, dev = 0;
     FS_OK(hipGetDevice(&dev));
@@ -973,6 +1018,7 @@ static int fsm_grids(FsmDev *fd) {
     fd->sized_S = fd->S;
     fd->sized_ns = fd->ns;
     fd->sized_K = fd->K;
+    fd->sized_sco = fd->sco;
     return HH_OK;
 }
 
@@ -984,6 +1030,23 @@ static int ws_need(FsmWs *ws, size_t need) {
     const size_t sz = need + need / 8;
     if (hipMalloc(&ws->p, sz) != hipSuccess) return HH_ERR_NOMEM;
     ws->size = sz;
+    FS_OK(hipMemset(ws->p, 0, 64));   // the status word; k_fscan2 clears it after each decode
+    return HH_OK;
+}
+
+void fsm_ws_free(FsmWs *ws) {
+    if (ws->p) (void)hipFree(ws->p);
+    if (ws->h_res) (void)hipHostFree(ws->h_res);
+    memset(ws, 0, sizeof(*ws));
+}
+
+static int ws_side(FsmWs *ws) {
+    if (ws->h_res) return HH_OK;
+    if (hipHostMalloc((void **)&ws->h_res, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+        ws->h_res = nullptr;
+        return HH_ERR_NOMEM;
+    }
+    FS_OK(hipHostGetDevicePointer((void **)&ws->d_res, ws->h_res, 0));
     return HH_OK;
 }
 
@@ -1027,14 +1090,18 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     wk.dbg = fd->dbg;
     FsmTab tab = {fd->ct, fd->b1, fd->tsym, fd->et, fd->er};
     const uint32_t sw = fd->S / 32;
-    FS_OK(hipMemsetAsync(wk.flags, 0, 64, st));
 #ifdef HH_DIAG
     if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, 16 * sizeof(uint64_t), st));
 #endif
+    rc = ws_side(ws);
+    if (rc) return rc;
+    (void)h_flags;
     FS_OK(hipEventRecord(ev[0], st));
     {
         // tiles [0, nc) whose regions and next region end before the stream,
-        // then the last ones (TAIL)
+        // then the last ones (TAIL).  (The tail launches on a second stream
+        // beside the main ones measured slower: the cross-stream waits cost
+        // more than the overlap saved, 0.155 -> 0.18 ms at 64 MiB.)
         const uint64_t S = fd->S;
         const uint64_t nc = bits > TB + S ? std::min<uint64_t>((bits - S - 1) / TB, nt) : 0;
         if (nc) {
@@ -1053,7 +1120,7 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     FS_OK(hipEventRecord(ev[1], st));
     hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk);
     FS_OK(hipGetLastError());
-    hipLaunchKernelGGL(k_fscan2, dim3(1), dim3(1024), 0, st, geo, wk, nblk);
+    hipLaunchKernelGGL(k_fscan2, dim3(1), dim3(1024), 0, st, geo, wk, nblk, ws->d_res);
     FS_OK(hipGetLastError());
     FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
@@ -1063,31 +1130,31 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
         if (ne > emit_from) {
             const uint64_t nwg = (ne - emit_from + ew - 1) / ew;
             const uint32_t ge = (uint32_t)(nwg < fd->grid_e ? nwg : fd->grid_e);
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch()), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch(), fd->sco), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne,
                                (uint32_t)lds_emf(fd));
             FS_OK(hipGetLastError());
         }
         if (ne < nt) {
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, true, 1), dim3((unsigned)((nt - ne + ew1 - 1) / ew1)), dim3(64 * ew1),
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, true, 1, false), dim3((unsigned)((nt - ne + ew1 - 1) / ew1)), dim3(64 * ew1),
                                lds_emf(fd), st, (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt,
                                (uint32_t)lds_emf(fd));
             FS_OK(hipGetLastError());
         }
     }
     FS_OK(hipEventRecord(ev[3], st));
-    FS_OK(hipMemcpyAsync(h_flags, wk.flags, 64, hipMemcpyDeviceToHost, st));
     FS_OK(hipStreamSynchronize(st));
-    const uint32_t fl = h_flags[0];
-    *total = (uint64_t)h_flags[2] | ((uint64_t)h_flags[3] << 32);
-    *leave = h_flags[4];
-    *entry = h_flags[5];
+    const volatile uint32_t *res = ws->h_res;
+    const uint32_t fl = res[0];
+    *total = (uint64_t)res[2] | ((uint64_t)res[3] << 32);
+    *leave = res[4];
+    *entry = res[5];
     if (emit_from >= nt) *total = 0;
     (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
     (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
     (void)hipEventElapsedTime(&ms[2], ev[2], ev[3]);
     if (fl & FF_FAIL) return HH_NOSYNC;
-    if (*total > cap || (fl & FF_OVER)) return HH_ERR_CAPACITY;
+    if (*total > cap) return HH_ERR_CAPACITY;
     return HH_OK;
 }
 

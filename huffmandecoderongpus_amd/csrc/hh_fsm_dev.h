@@ -19,7 +19,8 @@ struct FsmDev {
     uint8_t *tsym;
     uint64_t *et, *er;
     // persistent grids (workgroups), sized by the occupancy API for S / ns
-    uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K;
+    uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K, sized_sco;
+    uint32_t sco;            // k_emf's static copy-out (every tile output <= 16 KiB by the tree)
     uint64_t *dbg;           // HH_DIAG builds: phase cycles of k_cnt (16 x u64, the decoder's)
 };
 
@@ -33,11 +34,15 @@ struct FsmDev {
 struct FsmWs {
     void *p;
     size_t size;
+    // the decode's results (status, total, leave / entry state), written by
+    // k_fscan2 straight into host-mapped memory: no copy, no memset per decode
+    uint32_t *h_res, *d_res;
 };
+void fsm_ws_free(FsmWs *ws);
 int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
                hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms);
-int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G);
+int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen);
 bool fsm_k_fits(const hh_fsm_tables *F);     // 7-bit emission steps fit beside their staging
 void fsm_free(FsmDev *fd);
 int fsm_debug_arrays(const FsmWs *ws, uint64_t nt, uint32_t *rec, uint32_t *fx, int32_t *tsum, uint32_t *xs);

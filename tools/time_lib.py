@@ -71,6 +71,11 @@ if os.environ.get("HH_DIAG") == "fsm":     # a -DHH_DIAG build: k_cnt phase cycl
     res["cnt_walk_tiles"] = buf[9]
     res["cnt_walk_rounds"] = buf[10]
     res["cnt_cycles_per_tile"] = round(tot / max(buf[8], 1), 1)
+    ecyc = [buf[i] for i in range(4, 8)]
+    etot = sum(ecyc) or 1
+    res["emf_phase_frac"] = {n: round(ecyc[i] / etot, 3) for n, i in
+                             (("prologue", 0), ("region", 1), ("edges", 2), ("copyout", 3))}
+    res["emf_cycles_per_tile"] = round(etot / max(buf[8], 1), 1)
 elif os.environ.get("HH_DIAG"):            # a -DHH_DIAG build: phase cycles and walk lengths
     import ctypes as C
     buf = (C.c_uint64 * 16)()
