@@ -902,10 +902,18 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
                     }
                     __builtin_amdgcn_raw_buffer_store_b8(sb[q], ors, (int)(pb ? q : 0x40000000u), 0, 0);
                 } else {
-                    for (uint32_t i = j; i < nq; i += 64) {
-                        const uint32_t lo = 16 * i;
-                        if (lo >= a0[x] && lo + 16 <= end)
-                            __builtin_nontemporal_store(*(const u32x4 *)(sb + lo), (u32x4 *)(gb + lo));
+                    // four blocks per lane per pass: their LDS reads issued
+                    // together, one wait, then their stores
+                    for (uint32_t i0 = j; i0 < nq; i0 += 256) {
+                        u32x4 v[4];
+#pragma unroll
+                        for (uint32_t u = 0; u < 4; u++)   // (unconditional: past the tile's bytes they read
+                            v[u] = *(const u32x4 *)(sb + 16 * (i0 + 64 * u));   // what is never stored)
+#pragma unroll
+                        for (uint32_t u = 0; u < 4; u++) {
+                            const uint32_t lo = 16 * (i0 + 64 * u);
+                            if (lo >= a0[x] && lo + 16 <= end) __builtin_nontemporal_store(v[u], (u32x4 *)(gb + lo));
+                        }
                     }
                     if (pb) gb[q] = sb[q];
                 }
