@@ -45,7 +45,7 @@
 
 #define NR 64                 // regions per tile (a wave)
 #ifndef HH_CW
-#define HH_CW 12
+#define HH_CW 16
 #endif
 #define CW HH_CW               // k_cnt: waves per workgroup
 #ifndef HH_CNT_PNX
@@ -242,6 +242,10 @@ __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_
             const uint32_t e = ct_at(lds, s, rbyte<SW>(w, k));
             s = e;
             c += e & 15u;
+            // (the count added at its step: left to the scheduler, the adds
+            // sink to the end of the chain and every step's entry stays live
+            // -- 32 registers, the difference between 24 and 32 waves per CU)
+            asm volatile("" : "+v"(c));
         }
     }
     s &= 0xfe00u;
@@ -452,7 +456,7 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
 }
 
 #ifndef HH_CNT_WAVES
-#define HH_CNT_WAVES 6        // k_cnt: waves per SIMD the register budget is cut for (24 per CU: 2 workgroups of 12)
+#define HH_CNT_WAVES 8        // k_cnt: waves per SIMD the register budget is cut for (32 per CU: 2 workgroups of 16)
 #endif
 template <uint32_t SW, bool TAIL>
 __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
