@@ -463,6 +463,9 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
 // the region it walks (from G bits before it, for the heads of regions that
 // were not decoded, to a halo past it) at LDS index (q * HH_WALK_T + lane).
 // The lane's record replaces k_front's placeholder.
+// The merge/delta rule here must stay the one of hh_walk_exits (hh_algo.h),
+// which the emulator checks against the mask walk: a change to either is a
+// change to both (the GPU parity tests with HH_FLAG_LEGACY cover this copy).
 // ---------------------------------------------------------------------------
 #ifndef HH_WALK_T
 #define HH_WALK_T 256   // lanes per k_walk workgroup (64: +0.05 ms; 512: same)
@@ -1572,10 +1575,26 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     if (d->G > HH_GMAX || d->G + 32 > d->S) d->G = 0;
     // the state machine (trees of at most HH_FSM_MAXS internal nodes)
     fsm_free(&d->fsm);
-    // emission steps of 7 bits when the tables leave the staging room
-    // (fsm_k_fits), else 6 (HH_FSM_K: experiments)
+    // emission steps of 7 bits when their tables leave room for 16 stagings
+    // of the expected tile output (fsm_k_fits), else 6 (smaller tables, more
+    // waves: E.coli-like codes of 2 bits fill 8 KiB per tile); HH_FSM_K:
+    // experiments.  Expected bits per symbol: the code lengths weighted by
+    // 2^-length (exact for a code built from a dyadic distribution).
+    double avg = 0.0;
+    {
+        uint32_t stk[64], dep[64], sp = 0;
+        stk[sp] = 0; dep[sp++] = 0;
+        while (sp) {
+            const uint32_t id = stk[--sp], dd = dep[sp];
+            const uint32_t e = d->ht->tree[id];
+            if ((e & HH_T_LEAF) || dd >= 62) { avg += dd * ldexp(1.0, -(int)dd); continue; }
+            stk[sp] = e & 0x7fffu; dep[sp++] = dd + 1;
+            stk[sp] = (e >> 15) & 0x7fffu; dep[sp++] = dd + 1;
+        }
+    }
+    const uint32_t est = avg > 0.0 ? (uint32_t)(64.0 * d->S / avg) : 64u * d->S;
     uint32_t Kf = getenv("HH_FSM_K") ? (uint32_t)atoi(getenv("HH_FSM_K")) : 0u;
-    if (!Kf && d->S && hh_fsm_build(d->ht, d->S, 7, d->ft) == HH_OK && fsm_k_fits(d->ft)) Kf = 7;
+    if (!Kf && d->S && hh_fsm_build(d->ht, d->S, 7, d->ft) == HH_OK && fsm_k_fits(d->ft, est)) Kf = 7;
     if (d->S && hh_fsm_build(d->ht, d->S, Kf ? Kf : 6, d->ft) == HH_OK) {
         uint32_t Gf = hh_fsm_pick_head(d->ht, d->S);
         if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) & ~7u;   // experiments

@@ -309,10 +309,15 @@ __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns) {
 #define CDIAG_ARGS
 #define CDIAG_PASS
 #endif
+// hin: lane 0's guess for region 0 when the caller has it (the previous
+// tile's lane-63 head, same wave: tiles in order), else HIN_NONE (computed
+// here from pv, the 16 bytes before the tile).  Returns lane 63's head (the
+// next tile's region-0 guess), as a row.
+#define HIN_NONE 0xffffffffu
 template <uint32_t SW, bool TAIL>
-__device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
-                                         const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
-                                         const uint32_t *nx, const uint32_t *pv CDIAG_ARGS) {
+__device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
+                                             const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
+                                             const uint32_t *nx, const uint32_t *pv, uint32_t hin CDIAG_ARGS) {
     constexpr uint32_t S = 32 * SW;
     const uint32_t j = threadIdx.x & 63u;
     const uint64_t TB = (uint64_t)NR * S, T0 = t * TB;
@@ -339,15 +344,22 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
         const uint32_t GB = geo.G >> 3;                   // (uniform)
         constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
         static_assert(HB % 4 == 0, "head bytes in whole words");
+        if (hin == HIN_NONE) {
 #pragma unroll
-        for (uint32_t k = 4 * SW - HB; k < 4 * SW; k++)
-            if (k >= 4 * SW - GB) {
-                const uint32_t q = k - (4 * SW - HB);
-                gs = ct_at(lds, gs, rbyte<SW>(w, k));
-                hp = ct_at(lds, hp, __builtin_amdgcn_ubfe(pv[q >> 2], 8 * (q & 3), 8));
-            }
+            for (uint32_t k = 4 * SW - HB; k < 4 * SW; k++)
+                if (k >= 4 * SW - GB) {
+                    const uint32_t q = k - (4 * SW - HB);
+                    gs = ct_at(lds, gs, rbyte<SW>(w, k));
+                    hp = ct_at(lds, hp, __builtin_amdgcn_ubfe(pv[q >> 2], 8 * (q & 3), 8));
+                }
+            hp &= 0xfe00u;
+        } else {
+#pragma unroll
+            for (uint32_t k = 4 * SW - HB; k < 4 * SW; k++)
+                if (k >= 4 * SW - GB) gs = ct_at(lds, gs, rbyte<SW>(w, k));
+            hp = hin;
+        }
         gs &= 0xfe00u;
-        hp &= 0xfe00u;
     }
     CDIAG_STAMP(0);
     const uint32_t gup = shfl_up1(gs);              // (cross-lane ops with every lane active)
@@ -452,6 +464,7 @@ __device__ __forceinline__ void cnt_tile(const uint8_t *lds, const hh_fsm_view &
     }
     wk.fx[(t + 1) * FX_W + (j & (FX_W - 1))] = fxv;   // ((ntiles + 1) x FX_W words: the last tile's too)
     wk.xs[t] = x | fail << 31;                        // (bit 31: chains that did not meet, k_fscan reports it)
+    return (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
     CDIAG_STAMP(3);
 }
 
@@ -475,8 +488,14 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     const uint64_t TB = (uint64_t)NR * S;
     // tile indices fit 32 bits (2^32 tiles of >= 512 bytes); uniform, kept
     // in scalar registers
-    const uint32_t nwv = gridDim.x * CW, te = (uint32_t)t1;
-    uint32_t t = (uint32_t)t0 + blockIdx.x * CW + wv;
+    // each wave counts a contiguous run of tiles, in order (TAIL launches: a
+    // tile per wave): lane 0's region-0 guess of a tile is then the previous
+    // tile's lane-63 head, so only a run's first tile computes it
+    const uint32_t nwv = gridDim.x * CW, te = (uint32_t)t1, gw = blockIdx.x * CW + wv;
+    const uint32_t run = TAIL ? 1u : ((uint32_t)(t1 - t0) + nwv - 1) / nwv;
+    uint32_t t = TAIL ? (uint32_t)t0 + gw : (uint32_t)t0 + gw * run;
+    const uint32_t tend = TAIL ? te : (t + run < te ? t + run : te);
+    const uint32_t tstep = TAIL ? nwv : 1u;
     // the next tile's words are loaded one tile ahead: region j's and region
     // j+1's (used only by walks; waiting for them at the walk, behind the
     // previous tile's stores, cost as much as the walks themselves)
@@ -499,8 +518,9 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     };
     CDIAG_DECL
     if (t == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
-    if (t < te) prefetch(t);
-    for (; t < te; t += nwv) {
+    if (t < tend) prefetch(t);
+    uint32_t hin = HIN_NONE;
+    for (; t < tend; t += tstep) {
         t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
         uint32_t w[SW], nx[SW], pv[HB / 4];
 #pragma unroll
@@ -510,8 +530,9 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
         }
 #pragma unroll
         for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
-        prefetch(t + nwv < te ? t + nwv : t);
-        cnt_tile<SW, TAIL>(smem, F, g, geo, wk, (uint64_t)t, w, nx, pv CDIAG_PASS);
+        prefetch(t + tstep < tend ? t + tstep : t);
+        const uint32_t h63 = cnt_tile<SW, TAIL>(smem, F, g, geo, wk, (uint64_t)t, w, nx, pv, hin CDIAG_PASS);
+        hin = TAIL ? HIN_NONE : (uint32_t)__builtin_amdgcn_readfirstlane((int)h63);
     }
     CDIAG_FLUSH(wk.dbg);
 }
@@ -968,9 +989,11 @@ static size_t lds_cnt(const FsmDev *fd) { return cnt_tab_bytes(fd->ns); }
 #define EMF_LDS (160u * 1024u)
 static size_t lds_emf(const FsmDev *) { return EMF_LDS; }
 
-// 7-bit emission steps when their tables leave room for 16 stagings of 4 KiB
-bool fsm_k_fits(const hh_fsm_tables *F) {
-    return F->K == 7 && emf_tab_bytes(F->ns, 7, F->r) + 16u * 4096u <= EMF_LDS;
+// 7-bit emission steps when their tables leave room for 16 stagings of the
+// expected tile output
+bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile) {
+    const uint64_t need = ((uint64_t)est_tile + 16u + 8u + 15u) & ~15ull;   // (the stagings are sized at run time)
+    return F->K == 7 && emf_tab_bytes(F->ns, 7, F->r) + 16u * need <= EMF_LDS;
 }
 
 void fsm_free(FsmDev *fd) {

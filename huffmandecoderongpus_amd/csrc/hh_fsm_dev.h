@@ -43,7 +43,7 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
                hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms);
 int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen);
-bool fsm_k_fits(const hh_fsm_tables *F);     // 7-bit emission steps fit beside their staging
+bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile);   // 7-bit steps leave room for 16 stagings
 void fsm_free(FsmDev *fd);
 int fsm_debug_arrays(const FsmWs *ws, uint64_t nt, uint32_t *rec, uint32_t *fx, int32_t *tsum, uint32_t *xs);
 
