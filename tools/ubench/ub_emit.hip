@@ -7,6 +7,9 @@
 //   mode 1: the kernel's aligned-dword store with shift/spill every step
 //   mode 2: one unaligned 4-byte store at the run's byte offset every step
 //   mode 3: as 2, u64 accumulation, a store every second step
+//   mode 4: mode 1 with the store exec-masked to full dwords
+//   mode 6: pairs of steps, two dwords stored per pair (ds_write2_b32)
+//   mode 7: mode 1's stores into lane-private columns (conflict-free)
 // Tiles per wave and waves per workgroup are arguments; one workgroup per CU.
 // Build: hipcc -O3 --offload-arch=gfx950 -o /tmp/ub_emit tools/ubench/ub_emit.hip
 #include <hip/hip_runtime.h>
@@ -38,6 +41,8 @@ __global__ __launch_bounds__(1024) void k_emit(const uint64_t *gt, uint32_t tile
         uint32_t row = (w[0] % NS) << (K + 3);
         const uint32_t base = tab + wv * obw + j * 57;
         uint32_t o = base, wd = base & ~3u, sh = (base & 3u) * 8u, a = 0;
+        uint32_t cw = tab + wv * obw + j * 4;
+        if (MODE == 7) sh = 0;
         uint64_t a64 = 0;
         uint32_t sh64 = 0;
 #pragma unroll
@@ -71,6 +76,38 @@ __global__ __launch_bounds__(1024) void k_emit(const uint64_t *gt, uint32_t tile
                 a = full ? sp : an;
                 wd += full ? 4u : 0u;
                 sh = u & 31u;
+            } else if (MODE == 6) {
+                // pairs of steps: the pair's bytes (<= 8) shifted into the
+                // open dword; two dwords stored per pair (ds_write2_b32)
+                if ((k & 1) == 0) {
+                    a64 = lo;
+                    sh64 = hi & 255u;
+                } else {
+                    const uint64_t pb = a64 | ((uint64_t)lo << sh64);   // the pair's bytes
+                    const uint32_t nb = sh64 + (hi & 255u);             // their bits
+                    const uint32_t p0 = (uint32_t)pb, p1 = (uint32_t)(pb >> 32);
+                    const uint32_t v0 = (p0 << sh) | a;
+                    const uint32_t v1 = sh ? __builtin_amdgcn_alignbit(p1, p0, 32u - sh) : p1;
+                    const uint32_t v2 = sh ? p1 >> (32u - sh) : 0u;
+                    uint32_t *q = (uint32_t *)(smem + wd);
+                    q[0] = v0;
+                    q[1] = v1;
+                    const uint32_t u = sh + nb, full = u >> 5;
+                    a = full == 0 ? v0 : full == 1 ? v1 : v2;
+                    wd += 4u * full;
+                    sh = u & 31u;
+                }
+            } else if (MODE == 7) {
+                // mode 1's dword logic in a lane-private column (dword i of
+                // lane j at (i * 64 + j) * 4): no bank shared within a group
+                const uint32_t u = sh + (hi & 255u);
+                const uint32_t an = (lo << sh) | a;
+                const uint32_t sp = __builtin_amdgcn_alignbit(0u, lo, (0u - sh) & 31u);
+                *(uint32_t *)(smem + cw) = an;
+                const bool full = u >= 32;
+                a = full ? sp : an;
+                cw += full ? 256u : 0u;
+                sh = u & 31u;
             } else if (MODE == 5) {
                 // 64-bit accumulator, a dword stored when 4 bytes are ready
                 a64 |= (uint64_t)lo << sh64;
@@ -91,7 +128,7 @@ __global__ __launch_bounds__(1024) void k_emit(const uint64_t *gt, uint32_t tile
                 }
             }
         }
-        acc += a + o + wd + (uint32_t)a64;
+        acc += a + o + wd + (uint32_t)a64 + cw;
     }
     __syncthreads();
     if (tid < 64) acc += *(const uint32_t *)(smem + tab + tid * 4);
@@ -122,10 +159,10 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    void (*ks[6])(const uint64_t *, uint32_t, uint32_t *, uint32_t) = {k_emit<0>, k_emit<1>, k_emit<2>, k_emit<3>,
-                                                                       k_emit<4>, k_emit<5>};
-    for (int m = 0; m < 6; m++) {
-        if (m == 2 || m == 3) continue;
+    void (*ks[8])(const uint64_t *, uint32_t, uint32_t *, uint32_t) = {k_emit<0>, k_emit<1>, k_emit<2>, k_emit<3>,
+                                                                       k_emit<4>, k_emit<5>, k_emit<6>, k_emit<7>};
+    for (int m = 0; m < 8; m++) {
+        if (m == 2 || m == 3 || m == 5) continue;
         for (int rep = 0; rep < 3; rep++) {
             CK(hipEventRecord(e0));
             hipLaunchKernelGGL(ks[m], dim3(ncu), dim3(64 * waves), lds, 0, gt, tiles, sink, obw);
