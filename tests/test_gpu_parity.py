@@ -512,13 +512,15 @@ def test_eight_shards_of_the_8gib_stream():
         torch.cuda.empty_cache()
 
 
-def _shard_rank(rank, world, port, mib, q):
+def _shard_rank(rank, world, port, mib, q, backend="gloo"):
     import torch
     import torch.distributed as dist
     import huffmandecoderongpus_amd as H
     from huffmandecoderongpus_amd import shard, synth
     try:
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}",
+        if backend == "nccl":
+            torch.cuda.set_device(0)
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}",
                                 rank=rank, world_size=world)
         torch.cuda.set_device(0)
         hf, text = synth.load_source(os.path.join(ROOT, "files"))
@@ -563,6 +565,27 @@ def test_shard_job_two_ranks_one_gpu():
         assert ok is True, (rank, ok)
         assert n > 0
     assert got[1][3] > 0          # rank 1 decoded a prologue
+
+
+def test_shard_job_over_rccl_one_rank():
+    """The same ShardJob path over RCCL (backend "nccl"), one rank on GPU 0:
+    the settle exchange and the output all-gather run as RCCL collectives on
+    device tensors (all_gather, all_gather_into_tensor) -- the code the
+    multi-GPU bench runs on N GPUs (RCCL refuses two ranks on one GPU)."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_shard_rank, args=(0, 1, port, 32, q, "nccl"))
+    p.start()
+    rank, ok, n, pro = q.get(timeout=300)
+    p.join(timeout=60)
+    assert ok is True, ok
+    assert n > 0 and pro == 0
 
 
 @pytest.mark.parametrize("name", ["hello", "paper1", "news", "kjv.txt", "E.coli"])
