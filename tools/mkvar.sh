@@ -1,5 +1,5 @@
 # Build a variant of libhiphuff.so with extra compile flags for same-box A/B
-# (tools/gpu_walkab.sh): bash tools/mkvar.sh NAME "-DFOO=1 ..." -> build/var/NAME.so
+# (tools/gpu_ab.sh): bash tools/mkvar.sh NAME "-DFOO=1 ..." -> build/var/NAME.so
 set -e
 cd "$(dirname "$0")/.."
 N=$1; shift

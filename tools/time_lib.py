@@ -1,4 +1,4 @@
-"""A/B timing (tools/gpu_walkab.sh, tools/gpu_envab.sh): the decode pipeline on the synthetic stream with
+"""A/B timing (tools/gpu_ab.sh): the decode pipeline on the synthetic stream with
 the library named by HIPHUFF_LIB (default: the in-tree build); prints one
 JSON line with the median device time of each kernel phase over N runs and
 whether the output matched the tiled text.
