@@ -134,7 +134,8 @@ def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, s
             "compressed_bytes": C, "decoded_bytes": n_want,
             "roofline_frac": round(ach / HBM_PEAK_GBS, 4),
             "fast_path": all(s["exact_fallback"] == 0 for s in st),
-            "fixed_length_path": all(s["fixed_length"] == 1 for s in st)}
+            "fixed_length_path": all(s["fixed_length"] == 1 for s in st),
+            "state_machine_path": all(s["state_machine"] == 1 for s in st)}
 
 
 def evaluate_scope(H, hf, payload, bits: int, n_want: int, reps: int, check=None) -> dict:
@@ -341,6 +342,7 @@ def main():
                      "ms_emit": phases["emit"]},
         "decoded_MBps_device": round(D_bytes / (ms_dev * 1e-3) / 1e6, 1),
         "fast_path": fast,
+        "state_machine_path": all(s["state_machine"] == 1 for s in dev_ms),
     }
     res.update(extra)
     if world == 1:
