@@ -643,7 +643,9 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
 // every step (a dword is stored again until it is full: no branch).  The
 // unused bytes of every stored dword are zero: a dword shared with the
 // neighbouring runs is repaired by OR afterwards (emf_edges).
+#ifndef EMF_KE
 #define EMF_KE 8          // steps within which the first dword is captured
+#endif
 template <uint32_t K>
 struct EmfChain {
     uint32_t row, wd0, wd, sh, a, fw, wdk;
