@@ -386,6 +386,20 @@ def main():
                                     ks, 2))
         del out_i, iid
         torch.cuda.empty_cache()
+        # a byte alphabet: Huffman code over all 256 byte values (255 states,
+        # the state machine's 7-bit count steps over 224-bit regions)
+        byt = synth.byte_stream(target, device=dev)
+        dec_b = H.Decoder(local)
+        dec_b.set_tree(byt.tree)
+        out_b = torch.empty(byt.decoded_bytes + 4096, dtype=torch.uint8, device=dev)
+        more.append(device_workload(f"synthetic {a.size_mib} MiB byte-alphabet .huff (256-symbol Huffman "
+                                    f"code, Zipf s={synth.ZIPF_S} byte frequencies, splitmix64 seed "
+                                    f"{synth.BYTE_SEED:#x})", dec_b, byt.data, byt.bits, out_b,
+                                    byt.decoded_bytes,
+                                    lambda o: bool(torch.equal(o[:byt.decoded_bytes], byt.syms)), ks, 2))
+        dec_b.close()
+        del out_b, byt
+        torch.cuda.empty_cache()
         res["workloads"] = more
         # evaluate() scope: kjv.txt.huff itself, and the headline 1 GiB stream from host memory
         ev = {"kjv.txt": evaluate_scope(H, hf, hf.payload, hf.bits, hf.uncompressedsize, 20,

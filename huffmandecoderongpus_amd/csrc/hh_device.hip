@@ -465,7 +465,8 @@ __global__ __launch_bounds__(64 * HH_FW, HH_FRONT_MINB) void k_front(const uint3
 // The lane's record replaces k_front's placeholder.
 // The merge/delta rule here must stay the one of hh_walk_exits (hh_algo.h),
 // which the emulator checks against the mask walk: a change to either is a
-// change to both (the GPU parity tests with HH_FLAG_LEGACY cover this copy).
+// change to both (the GPU parity tests with HH_FLAG_LEGACY cover this copy:
+// test_walk_bound_and_deferral_lists, test_fixture_legacy_pipeline).
 // ---------------------------------------------------------------------------
 #ifndef HH_WALK_T
 #define HH_WALK_T 256   // lanes per k_walk workgroup (64: +0.05 ms; 512: same)
@@ -1545,6 +1546,13 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     d->tab.l2_used = d->ht->l2_used;
     d->tab.tree_lds = d->ht->tree_used;
     d->S = pick_region_bits(d->ht, d->cfg.lane_bits);
+    // trees of more than 127 states: the state machine counts in 7-bit steps
+    // over 224-bit regions (hh_fsm.h), and the decoder's tiles are its tiles
+    // (tile_bits, shards, the evaluate() chunks)
+    if (!(d->cfg.flags & HH_FLAG_LEGACY) && d->cfg.lane_bits == 0) {
+        const uint32_t Sf = hh_fsm_region_bits(hh_fsm_nstates(d->ht), (uint32_t)d->ht->len_gcd, d->S);
+        if (Sf) d->S = Sf;
+    }
     // a complete fixed-length code: every L-bit window is one symbol
     d->fixed_len = 0;
     const int L = d->ht->fixed_len;
@@ -1573,7 +1581,7 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     d->G = hh_pick_overlap(d->ht);
     if (getenv("HH_OVERLAP")) d->G = (uint32_t)atoi(getenv("HH_OVERLAP")) & ~31u;   // experiments
     if (d->G > HH_GMAX || d->G + 32 > d->S) d->G = 0;
-    // the state machine (trees of at most HH_FSM_MAXS internal nodes)
+    // the state machine (trees of at most HH_FSM_MAXS = 255 internal nodes)
     fsm_free(&d->fsm);
     // emission steps of 7 bits when their tables leave room for 16 stagings
     // of the expected tile output (fsm_k_fits), else 6 (smaller tables, more
@@ -1596,8 +1604,8 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     uint32_t Kf = getenv("HH_FSM_K") ? (uint32_t)atoi(getenv("HH_FSM_K")) : 0u;
     if (!Kf && d->S && hh_fsm_build(d->ht, d->S, 7, d->ft) == HH_OK && fsm_k_fits(d->ft, est)) Kf = 7;
     if (d->S && hh_fsm_build(d->ht, d->S, Kf ? Kf : 6, d->ft) == HH_OK) {
-        uint32_t Gf = hh_fsm_pick_head(d->ht, d->S);
-        if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) & ~7u;   // experiments
+        uint32_t Gf = hh_fsm_pick_head(d->ht, d->S, d->ft->cb);
+        if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) / d->ft->cb * d->ft->cb;   // experiments
         if (Gf > d->S) Gf = 0;
         const int urc = fsm_upload(&d->fsm, d->ft, Gf, (uint32_t)d->ht->minlen);
         d->fsm.dbg = d->d_dbg;

@@ -15,16 +15,19 @@
  * pointer doubling, makebigtable.cl:10-40).
  *
  * States are numbered 0..ns-1 (internal nodes of the compact tree, BFS
- * order, root first); ns <= HH_FSM_MAXS keeps a state's table row (state
- * << 9 bytes) in 16 bits.
+ * order, root first), ns <= HH_FSM_MAXS (255: any tree over a byte alphabet
+ * has at most 255 internal nodes).  The count table's step width CB depends
+ * on ns so that an entry (next state's row offset | count) stays 16 bits:
+ * CB = 8 for ns <= 127 (row = state << 9), CB = 7 for larger trees (row =
+ * state << 8; regions of S = 224 bits, 32 steps).
  *
- *   ct[s * 256 + b]   u16: 8-bit steps (count pass): the state after the 8
- *                     stream bits b (stream bit p in bit 0, the reference's
- *                     LSB-first order, decodeallbits.cl:23) << 9, i.e. its
- *                     row's byte offset | the codes completed on the way
- *                     (bits 0..3): the next lookup's address is
- *                     (entry & 0xfe00) | b << 1
- *   b1[s * 2 + bit]   u32: 1-bit steps (the stream's last partial byte):
+ *   ct[s << CB | v]   u16: CB-bit steps (count pass): the state after the CB
+ *                     stream bits v (stream bit p in bit 0, the reference's
+ *                     LSB-first order, decodeallbits.cl:23) << (CB + 1),
+ *                     i.e. its row's byte offset | the codes completed on the
+ *                     way (bits 0..3): the next lookup's address is
+ *                     (entry & row mask) | v << 1
+ *   b1[s * 2 + bit]   u32: 1-bit steps (the stream's last partial step):
  *                     next state | completed << 8 | the symbol << 16
  *   tsym[s]           the sym byte of the state's node: the symbol the
  *                     reference emits for a code cut off by the end of the
@@ -36,6 +39,7 @@
  *                     completes up to 3 (K = 6) or 4 (K = 7, 4) symbols
  *       bits 32..39   8 x the number of symbols (the output shift)
  *       bits 47..63   the next state's row in et, in bytes: next << (K + 3)
+ *                     (17 bits: K = 7 only for ns <= 127)
  *   er[s << r | v]    u64: the r-bit step that ends a region of S bits when K
  *                     does not divide S (r = S mod K, 0: none); same layout,
  *                     rows in et units
@@ -45,13 +49,16 @@
 
 #include <stdint.h>
 
-#define HH_FSM_MAXS 127
+#define HH_FSM_MAXS 255
+#define HH_FSM_MAXS8 127    /* largest ns with 8-bit count steps */
+#define HH_FSM_S7 224       /* region bits with 7-bit count steps */
 
 typedef struct {
     uint32_t ns;              /* states (internal nodes)                      */
     uint32_t K;               /* emission step bits                           */
     uint32_t r;               /* remainder step bits of a region (S mod K)    */
     uint32_t S;               /* region bits the remainder table is built for */
+    uint32_t cb;              /* count step bits: 8 (ns <= 127) or 7          */
     uint16_t ct[HH_FSM_MAXS * 256];
     uint32_t b1[HH_FSM_MAXS * 2];
     uint8_t tsym[HH_FSM_MAXS + 1];
@@ -64,7 +71,7 @@ typedef struct {
 #define HH_FSM_ET_NSYM(e) ((uint32_t)((e) >> 35) & 31u)
 #define HH_FSM_ET_MAKE(syms, row, n) \
     ((uint64_t)(uint32_t)(syms) | (uint64_t)(8u * (uint32_t)(n)) << 32 | (uint64_t)(uint32_t)(row) << 47)
-#define HH_FSM_CT_NEXT(v) ((uint32_t)(v) >> 9)
+#define HH_FSM_CT_NEXT(v, cb) ((uint32_t)(v) >> ((cb) + 1))
 #define HH_FSM_CT_CNT(v) ((uint32_t)(v) & 15u)
 
 #ifdef __cplusplus
@@ -72,9 +79,14 @@ extern "C" {
 #endif
 /* Builds the state machine of the compact tree in T (hh_tables_build) for
  * regions of S bits, emission steps of K bits (6 or 7; 0: 6; a code of 1 bit
- * takes K = 4 whatever is asked).  HH_ERR_UNSUPPORTED when the tree has more
- * than HH_FSM_MAXS internal nodes. */
+ * takes K = 4 whatever is asked; trees of more than HH_FSM_MAXS8 internal
+ * nodes take at most 6).  Count steps of 8 bits when ns <= HH_FSM_MAXS8 and
+ * S is whole bytes, else of 7 bits (S a multiple of 7).  HH_ERR_UNSUPPORTED
+ * when the tree has more than HH_FSM_MAXS internal nodes or S does not fit
+ * the count step. */
 int hh_fsm_build(const void *T /* const hh_tables* */, uint32_t S, uint32_t K, hh_fsm_tables *F);
+/* The number of states (internal nodes) of the compact tree in T. */
+uint32_t hh_fsm_nstates(const void *T /* const hh_tables* */);
 #ifdef __cplusplus
 }
 #endif

@@ -189,16 +189,20 @@ __device__ __forceinline__ uint32_t rbits(const uint32_t *w, uint32_t q, uint32_
     if (o + n <= 32 || i + 1 >= SW) return __builtin_amdgcn_ubfe(w[i], o, n);
     return __builtin_amdgcn_alignbit(w[i + 1], w[i], o) & ((1u << n) - 1u);
 }
-// bits [q, q+K) of a region times 8: a byte offset into a row of the
-// emission table (compile-time q)
-template <uint32_t SW, uint32_t K>
-__device__ __forceinline__ uint32_t win8(const uint32_t *w, uint32_t q) {
-    constexpr uint32_t M = ((1u << K) - 1u) << 3;
-    if (q < 3) return (w[0] << (3 - q)) & M;
-    const uint32_t p = q - 3, i = p >> 5, o = p & 31;
-    if (o + K + 3 <= 32 || i + 1 >= SW) return (w[i] >> o) & M;
+// bits [q, q+N) of a region times 2^SH: a byte offset into a table row
+// (compile-time q)
+template <uint32_t SW, uint32_t N, uint32_t SH>
+__device__ __forceinline__ uint32_t winsh(const uint32_t *w, uint32_t q) {
+    constexpr uint32_t M = ((1u << N) - 1u) << SH;
+    if (q < SH) return (w[0] << (SH - q)) & M;
+    const uint32_t p = q - SH, i = p >> 5, o = p & 31;
+    if (o + N + SH <= 32 || i + 1 >= SW) return (w[i] >> o) & M;
     return __builtin_amdgcn_alignbit(w[i + 1], w[i], o) & M;
 }
+// bits [q, q+K) of a region times 8: a byte offset into a row of the
+// emission table
+template <uint32_t SW, uint32_t K>
+__device__ __forceinline__ uint32_t win8(const uint32_t *w, uint32_t q) { return winsh<SW, K, 3>(w, q); }
 // bit q of a region held in registers, q not a compile-time constant (rare paths)
 template <uint32_t SW>
 __device__ __forceinline__ uint32_t rbit_dyn(const uint32_t *w, uint32_t q) {
@@ -208,16 +212,31 @@ __device__ __forceinline__ uint32_t rbit_dyn(const uint32_t *w, uint32_t q) {
     return (x >> (q & 31)) & 1u;
 }
 
-// The count table at LDS address 0: a state is carried as its row's byte
-// offset (state << 9), an entry is the next row | the codes completed, so
-// the next lookup's address is one AND-OR of the entry and the byte.
-__device__ __forceinline__ uint32_t ct_at(const uint8_t *lds, uint32_t row, uint32_t b) {
-    return *(const uint16_t *)(lds + ((row & 0xfe00u) | (b << 1)));
+// The count table at LDS address 0: CB-bit steps (8 for trees of <= 127
+// states, 7 above: hh_fsm.h).  A state is carried as its row's byte offset
+// (state << (CB + 1)), an entry is the next row | the codes completed, so
+// the next lookup's address is one AND-OR of the entry and the step's bits
+// (times 2: u16 entries).
+template <uint32_t CB>
+struct CntFmt {
+    static constexpr uint32_t RS = CB + 1;                          // row = state << RS
+    static constexpr uint32_t RM = CB == 8 ? 0xfe00u : 0xff00u;     // the row bits of an entry
+};
+template <uint32_t CB>
+__device__ __forceinline__ uint32_t ct_at(const uint8_t *lds, uint32_t row, uint32_t off) {
+    return *(const uint16_t *)(lds + ((row & CntFmt<CB>::RM) | off));
 }
+// step k's table offset (its CB bits << 1) in a region held in registers
+template <uint32_t SW, uint32_t CB>
+__device__ __forceinline__ uint32_t cstep(const uint32_t *w, uint32_t k) {
+    if (CB == 8) return rbyte<SW>(w, k) << 1;
+    return winsh<SW, CB, 1>(w, CB * k);
+}
+template <uint32_t CB>
 __device__ __forceinline__ uint32_t b1_row(const uint32_t *b1, uint32_t row, uint32_t bit, uint32_t *c) {
-    const uint32_t v = b1[(row >> 9) * 2 + bit];
+    const uint32_t v = b1[(row >> CntFmt<CB>::RS) * 2 + bit];
     *c += (v >> 8) & 255u;
-    return (v & 255u) << 9;
+    return (v & 255u) << CntFmt<CB>::RS;
 }
 
 // The rare cross-tile fixer out of line: its registers do not add to the
@@ -232,14 +251,14 @@ __device__ __noinline__ int cnt_fix_next(const hh_fsm_view *F, const uint32_t *w
 // region's readable bits (S unless the stream ends inside it); only the TAIL
 // instantiations check it.
 // ---------------------------------------------------------------------------
-template <uint32_t SW, bool TAIL>
+template <uint32_t SW, bool TAIL, uint32_t CB>
 __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
                                                uint32_t s, uint32_t lim, uint32_t *n) {
     uint32_t c = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < 4 * SW; k++) {
-        if (!TAIL || 8 * k + 8 <= lim) {
-            const uint32_t e = ct_at(lds, s, rbyte<SW>(w, k));
+    for (uint32_t k = 0; k < 32 * SW / CB; k++) {
+        if (!TAIL || CB * k + CB <= lim) {
+            const uint32_t e = ct_at<CB>(lds, s, cstep<SW, CB>(w, k));
             s = e;
             c += e & 15u;
             // (the count added at its step: left to the scheduler, the adds
@@ -248,9 +267,9 @@ __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_
             asm volatile("" : "+v"(c));
         }
     }
-    s &= 0xfe00u;
+    s &= CntFmt<CB>::RM;
     if (TAIL)
-        for (uint32_t q = lim & ~7u; q < lim; q++) s = b1_row(b1, s, rbit_dyn<SW>(w, q), &c);   // the last partial byte
+        for (uint32_t q = lim / CB * CB; q < lim; q++) s = b1_row<CB>(b1, s, rbit_dyn<SW>(w, q), &c);   // the last partial step
     *n = c;
     return s;
 }
@@ -261,29 +280,30 @@ __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_
 // are masked off: a table read costs LDS cycles per distinct bank address of
 // its ACTIVE lanes, and most lanes do not walk).  Stops when every lane has
 // met.
-template <uint32_t SW, bool TAIL>
+template <uint32_t SW, bool TAIL, uint32_t CB>
 __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
                                             uint32_t &A, uint32_t &B, int32_t &d, uint32_t lim) {
+    constexpr uint32_t RM = CntFmt<CB>::RM;
     bool go = true;                                   // (uniform) some lane has not met yet
 #pragma unroll
-    for (uint32_t k = 0; k < 4 * SW; k++) {
-        if (go && (!TAIL || 8 * k + 8 <= lim)) {
+    for (uint32_t k = 0; k < 32 * SW / CB; k++) {
+        if (go && (!TAIL || CB * k + CB <= lim)) {
             if (!HH_WALK_MASK || A != B) {
-                const uint32_t x = rbyte<SW>(w, k);
-                const uint32_t ea = ct_at(lds, A, x), eb = ct_at(lds, B, x);
-                A = ea & 0xfe00u;
-                B = eb & 0xfe00u;
+                const uint32_t x = cstep<SW, CB>(w, k);
+                const uint32_t ea = ct_at<CB>(lds, A, x), eb = ct_at<CB>(lds, B, x);
+                A = ea & RM;
+                B = eb & RM;
                 d += (int32_t)(ea & 15u) - (int32_t)(eb & 15u);
             }
         }
         if ((k & HH_WALK_CHK) == HH_WALK_CHK && go) go = __ballot(A != B) != 0;
     }
     if (TAIL) {
-        for (uint32_t q = lim & ~7u; q < lim && A != B; q++) {
+        for (uint32_t q = lim / CB * CB; q < lim && A != B; q++) {
             const uint32_t x = rbit_dyn<SW>(w, q);
             uint32_t ca = 0, cb = 0;
-            A = b1_row(b1, A, x, &ca);
-            B = b1_row(b1, B, x, &cb);
+            A = b1_row<CB>(b1, A, x, &ca);
+            B = b1_row<CB>(b1, B, x, &cb);
             d += (int32_t)ca - (int32_t)cb;
         }
     }
@@ -294,8 +314,8 @@ __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *
 // tiles in which the stream ends (or whose next tile's region 0 holds the
 // end), launched on their own.
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns) {
-    return ((ns * 512u + ns * 8u + ns) + 15u) & ~15u;
+__host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns, uint32_t cb) {
+    return (((ns << (cb + 1)) + ns * 8u + ns) + 15u) & ~15u;
 }
 
 // One tile: w = region j's words, nx = region j+1's (lane 63: the next
@@ -314,11 +334,11 @@ __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns) {
 // here from pv, the 16 bytes before the tile).  Returns lane 63's head (the
 // next tile's region-0 guess), as a row.
 #define HIN_NONE 0xffffffffu
-template <uint32_t SW, bool TAIL>
+template <uint32_t SW, bool TAIL, uint32_t CB>
 __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
                                              const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
                                              const uint32_t *nx, const uint32_t *pv, uint32_t hin CDIAG_ARGS) {
-    constexpr uint32_t S = 32 * SW;
+    constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS, RM = CntFmt<CB>::RM;
     const uint32_t j = threadIdx.x & 63u;
     const uint64_t TB = (uint64_t)NR * S, T0 = t * TB;
     const uint64_t R = T0 + (uint64_t)j * S;
@@ -341,31 +361,37 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
         // over the previous region's last G bits -- uniform words (scalar
         // loads), a chain every lane runs alike (broadcast reads), interleaved
         // with its own head
-        const uint32_t GB = geo.G >> 3;                   // (uniform)
+        // head steps: the last G / CB count steps of the region; pv holds
+        // the HB bytes before the tile (lane 0's head reads the same step
+        // positions in them)
+        constexpr uint32_t NS = S / CB;
         constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
+        constexpr uint32_t HS = NS < HH_FSM_GMAX / CB ? NS : HH_FSM_GMAX / CB;   // head steps at most
         static_assert(HB % 4 == 0, "head bytes in whole words");
+        static_assert(CB * HS <= 8 * HB, "the head of region 0 within the bytes before the tile");
+        const uint32_t GS = geo.G / CB;                   // (uniform)
         if (hin == HIN_NONE) {
 #pragma unroll
-            for (uint32_t k = 4 * SW - HB; k < 4 * SW; k++)
-                if (k >= 4 * SW - GB) {
-                    const uint32_t q = k - (4 * SW - HB);
-                    gs = ct_at(lds, gs, rbyte<SW>(w, k));
-                    hp = ct_at(lds, hp, __builtin_amdgcn_ubfe(pv[q >> 2], 8 * (q & 3), 8));
+            for (uint32_t k = NS - HS; k < NS; k++)
+                if (k >= NS - GS) {
+                    gs = ct_at<CB>(lds, gs, cstep<SW, CB>(w, k));
+                    hp = ct_at<CB>(lds, hp, CB == 8 ? __builtin_amdgcn_ubfe(pv[(k - (NS - HS)) >> 2], 8 * ((k - (NS - HS)) & 3), 8) << 1
+                                                    : winsh<HB / 4, CB, 1>(pv, 8 * HB + CB * k - S));
                 }
-            hp &= 0xfe00u;
+            hp &= RM;
         } else {
 #pragma unroll
-            for (uint32_t k = 4 * SW - HB; k < 4 * SW; k++)
-                if (k >= 4 * SW - GB) gs = ct_at(lds, gs, rbyte<SW>(w, k));
+            for (uint32_t k = NS - HS; k < NS; k++)
+                if (k >= NS - GS) gs = ct_at<CB>(lds, gs, cstep<SW, CB>(w, k));
             hp = hin;
         }
-        gs &= 0xfe00u;
+        gs &= RM;
     }
     CDIAG_STAMP(0);
     const uint32_t gup = shfl_up1(gs);              // (cross-lane ops with every lane active)
-    const uint32_t sp = j ? gup : (t == 0 ? geo.in_state << 9 : hp);
+    const uint32_t sp = j ? gup : (t == 0 ? geo.in_state << RS : hp);
     uint32_t n;
-    uint32_t X = cnt_region<SW, TAIL>(lds, F.b1, w, sp, lim, &n);   // region j's exit (given its entry)
+    uint32_t X = cnt_region<SW, TAIL, CB>(lds, F.b1, w, sp, lim, &n);   // region j's exit (given its entry)
     // the stream ends in region j / in region j+1: the tail rule counts a
     // chain that is not at the root there (fsm_region, fsm_walk2)
     const bool endj = TAIL && lim > 0 && R + lim == geo.bits;
@@ -405,7 +431,7 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
         // of the rounds loop into 4 x SW live registers)
 #pragma unroll
         for (uint32_t k = 0; k < SW; k++) asm volatile("" : "+v"(nv[k]));
-        walk_region<SW, TAIL>(lds, F.b1, nv, A, B, dd, limn);
+        walk_region<SW, TAIL, CB>(lds, F.b1, nv, A, B, dd, limn);
         bool deep = false;
         if (want) {
             if (endn && A != B) dd += (int32_t)(A != 0) - (int32_t)(B != 0);   // tail rule
@@ -425,7 +451,7 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
     CDIAG_COUNT(0, 1);
     // records: region j entered in the state lane j-1 assumed last
     const uint32_t Eup = shfl_up1(E), dup = shfl_up1((uint32_t)d);
-    const uint32_t ent = (j ? Eup : sp) >> 9;
+    const uint32_t ent = (j ? Eup : sp) >> RS;
     const uint32_t cnt = (uint32_t)((int32_t)n + (j ? (int32_t)dup : 0));
     // the tile's stores are unconditional (every lane the same value where a
     // word is the tile's: one store instruction, no branch), so that the
@@ -433,7 +459,7 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
     // words, not for these stores to reach memory
     wk.rec[t * NR + j] = fsm_rec(ent, cnt);
     const int32_t sum = wave_sum((int32_t)cnt);
-    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63) >> 9;
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63) >> RS;
     wk.tsum[t] = sum;
     // the next tile's corrections (its region 0 assumed entered in the head
     // guess, lane 63's gs); lanes j and j + 8k store the same word
@@ -441,16 +467,16 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
     if (has_next) {
         const bool lst = __builtin_amdgcn_readlane((int)lost, 63) != 0;
         if (!lst) {
-            const uint32_t E63 = (uint32_t)__builtin_amdgcn_readlane((int)E, 63) >> 9;
+            const uint32_t E63 = (uint32_t)__builtin_amdgcn_readlane((int)E, 63) >> RS;
             const int32_t d63 = __builtin_amdgcn_readlane(d, 63);
-            const uint32_t g63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> 9;
+            const uint32_t g63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
             const bool walked = E63 != g63 || d63 != 0;      // (lane 63 walked into the next tile)
             fxv = (j & (FX_W - 1)) == 0 && walked ? fsm_fx(E63, d63) : 0u;
         } else {
             // rare: the chains meet beyond the next tile's region 0 (lane 0,
             // words from global memory)
             uint32_t f[FX_W], ok = 1;
-            const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> 9;
+            const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
             if (j == 0) ok = cnt_fix_next(&F, g, T0 + TB, S, geo.bits, x, h63, f);
             else
                 for (int i = 0; i < FX_W; i++) f[i] = 0;
@@ -471,20 +497,21 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
 #ifndef HH_CNT_WAVES
 #define HH_CNT_WAVES 8        // k_cnt: waves per SIMD the register budget is cut for (32 per CU: 2 workgroups of 16)
 #endif
-template <uint32_t SW, bool TAIL>
+template <uint32_t SW, bool TAIL, uint32_t CB>
 __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint64_t t0, uint64_t t1) {
+    static_assert((32 * SW) % CB == 0, "whole count steps per region");
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW;
     const uint32_t ns = geo.ns, tid = threadIdx.x, j = tid & 63u;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // (uniform: scalar tile index)
-    uint32_t *s_b1 = (uint32_t *)(smem + ns * 512);
+    uint32_t *s_b1 = (uint32_t *)(smem + (ns << (CB + 1)));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
-    for (uint32_t i = tid; i < ns * 128; i += blockDim.x) ((uint32_t *)smem)[i] = ((const uint32_t *)tab.ct)[i];
+    for (uint32_t i = tid; i < (ns << (CB - 1)); i += blockDim.x) ((uint32_t *)smem)[i] = ((const uint32_t *)tab.ct)[i];
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
     __syncthreads();
-    const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts};
+    const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts, CB};
     const uint64_t TB = (uint64_t)NR * S;
     // tile indices fit 32 bits (2^32 tiles of >= 512 bytes); uniform, kept
     // in scalar registers
@@ -531,7 +558,7 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
 #pragma unroll
         for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
         prefetch(t + tstep < tend ? t + tstep : t);
-        const uint32_t h63 = cnt_tile<SW, TAIL>(smem, F, g, geo, wk, (uint64_t)t, w, nx, pv, hin CDIAG_PASS);
+        const uint32_t h63 = cnt_tile<SW, TAIL, CB>(smem, F, g, geo, wk, (uint64_t)t, w, nx, pv, hin CDIAG_PASS);
         hin = TAIL ? HIN_NONE : (uint32_t)__builtin_amdgcn_readfirstlane((int)h63);
     }
     CDIAG_FLUSH(wk.dbg);
@@ -960,9 +987,12 @@ typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint
 typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t, uint32_t);
 
 #define FSM_SW_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
-static kcnt_t kcnt_for(uint32_t sw, bool tail) {
+static kcnt_t kcnt_for(uint32_t sw, bool tail, uint32_t cb) {
+    // 7-bit count steps: trees of more than 127 states, 224-bit regions only
+    if (cb == 7) return sw == HH_FSM_S7 / 32 ? (tail ? k_cnt<HH_FSM_S7 / 32, true, 7> : k_cnt<HH_FSM_S7 / 32, false, 7>) : nullptr;
+    if (cb != 8) return nullptr;
     switch (sw) {
-#define X(n) case n: return tail ? k_cnt<n, true> : k_cnt<n, false>;
+#define X(n) case n: return tail ? k_cnt<n, true, 8> : k_cnt<n, false, 8>;
         FSM_SW_CASES(X)
 #undef X
     default: return nullptr;
@@ -985,11 +1015,12 @@ static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sc
     }
 }
 
-static size_t lds_cnt(const FsmDev *fd) { return cnt_tab_bytes(fd->ns); }
+static size_t lds_cnt(const FsmDev *fd) { return cnt_tab_bytes(fd->ns, fd->cb); }
 // k_emf takes the whole LDS (one workgroup per CU) and sizes its stagings
 // from the largest tile output at run time
 #define EMF_LDS (160u * 1024u)
 static size_t lds_emf(const FsmDev *) { return EMF_LDS; }
+static_assert(EMF_LDS <= 160u * 1024u, "k_emf's LDS");
 
 // 7-bit emission steps when their tables leave room for 16 stagings of the
 // expected tile output
@@ -1011,24 +1042,32 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen) 
     fsm_free(fd);
     const uint32_t ns = F->ns;
     const uint32_t sw = F->S / 32;
-    if (F->S % 32 || sw < 2 || sw > 12 || G % 8 || G > HH_FSM_GMAX || G > F->S) return HH_ERR_UNSUPPORTED;
+    if (F->S % 32 || sw < 2 || sw > 12 || (F->cb != 8 && F->cb != 7) || G % F->cb || G > HH_FSM_GMAX || G > F->S)
+        return HH_ERR_UNSUPPORTED;
+    if (!kcnt_for(sw, false, F->cb)) return HH_ERR_UNSUPPORTED;
+    // the tables in LDS: k_cnt's count table; k_emf's emission tables plus
+    // at least one staging of the largest tile output the tree allows
+    // (k_emf sizes its stagings at run time, from this decode's largest)
+    const uint64_t tmax = (uint64_t)NR * F->S / (minlen ? minlen : 1u) + 1u;
+    if (cnt_tab_bytes(ns, F->cb) > 160u * 1024u / 2u ||
+        (uint64_t)emf_tab_bytes(ns, F->K, F->r) + ((tmax + 16u + 8u + 15u) & ~15ull) > EMF_LDS)
+        return HH_ERR_UNSUPPORTED;
     fd->ns = ns;
+    fd->cb = F->cb;
     fd->K = F->K;
     fd->r = F->r;
     fd->S = F->S;
     fd->G = G;
     // every tile's output is at most 64 S / minlen symbols (+ the tail rule's)
-    const uint64_t tmax = (uint64_t)NR * F->S / (minlen ? minlen : 1u) + 1u;
     // (measured no faster than the store loop -- the time moved from the
     // wait at the tile start into the stores -- so it is opt-in: HH_EMF_SCO)
     fd->sco = tmax + 16u + 8u + 15u <= (uint64_t)EMF_COI * 1024u && getenv("HH_EMF_SCO");
-    if (lds_emf(fd) > 160 * 1024 || lds_cnt(fd) > 160 * 1024) return HH_ERR_UNSUPPORTED;
-    FS_OK(hipMalloc(&fd->ct, (size_t)ns * 512));
+    FS_OK(hipMalloc(&fd->ct, (size_t)ns << (F->cb + 1)));
     FS_OK(hipMalloc(&fd->b1, (size_t)ns * 8));
     FS_OK(hipMalloc(&fd->tsym, (size_t)ns + 1));
     FS_OK(hipMalloc(&fd->et, (size_t)(ns << F->K) * 8));
     FS_OK(hipMalloc(&fd->er, (size_t)(ns << (F->r ? F->r : 1)) * 8));
-    FS_OK(hipMemcpy(fd->ct, F->ct, (size_t)ns * 512, hipMemcpyHostToDevice));
+    FS_OK(hipMemcpy(fd->ct, F->ct, (size_t)ns << (F->cb + 1), hipMemcpyHostToDevice));
     FS_OK(hipMemcpy(fd->b1, F->b1, (size_t)ns * 8, hipMemcpyHostToDevice));
     FS_OK(hipMemcpy(fd->tsym, F->tsym, (size_t)ns, hipMemcpyHostToDevice));
     FS_OK(hipMemcpy(fd->et, F->et, (size_t)(ns << F->K) * 8, hipMemcpyHostToDevice));
@@ -1038,10 +1077,11 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen) 
 }
 
 static int fsm_grids(FsmDev *fd) {
-    if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns && fd->sized_K == fd->K && fd->sized_sco == fd->sco)
+    if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns && fd->sized_K == fd->K && fd->sized_sco == fd->sco &&
+        fd->sized_cb == fd->cb)
         return HH_OK;
     const uint32_t sw = fd->S / 32;
-    const kcnt_t kc = kcnt_for(sw, false);
+    const kcnt_t kc = kcnt_for(sw, false, fd->cb);
     const kemf_t ke = kemf_for(sw, fd->K, false, emf_nch(), fd->sco);
     if (!kc || !ke) return HH_ERR_UNSUPPORTED;
     int pc = 0, pe = 0, ncu = 0, dev = 0;
@@ -1056,6 +1096,7 @@ static int fsm_grids(FsmDev *fd) {
     fd->sized_ns = fd->ns;
     fd->sized_K = fd->K;
     fd->sized_sco = fd->sco;
+    fd->sized_cb = fd->cb;
     return HH_OK;
 }
 
@@ -1144,12 +1185,12 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
         if (nc) {
             const uint64_t nwg = (nc + CW - 1) / CW;
             const uint32_t gc = (uint32_t)(nwg < fd->grid_c ? nwg : fd->grid_c);
-            hipLaunchKernelGGL(kcnt_for(sw, false), dim3(gc), dim3(64 * CW), lds_cnt(fd), st, (const uint32_t *)d_data,
+            hipLaunchKernelGGL(kcnt_for(sw, false, fd->cb), dim3(gc), dim3(64 * CW), lds_cnt(fd), st, (const uint32_t *)d_data,
                                geo, tab, wk, (uint64_t)0, nc);
             FS_OK(hipGetLastError());
         }
         if (nc < nt) {
-            hipLaunchKernelGGL(kcnt_for(sw, true), dim3((unsigned)((nt - nc + CW - 1) / CW)), dim3(64 * CW), lds_cnt(fd),
+            hipLaunchKernelGGL(kcnt_for(sw, true, fd->cb), dim3((unsigned)((nt - nc + CW - 1) / CW)), dim3(64 * CW), lds_cnt(fd),
                                st, (const uint32_t *)d_data, geo, tab, wk, nc, nt);
             FS_OK(hipGetLastError());
         }

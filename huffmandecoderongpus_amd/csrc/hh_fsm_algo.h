@@ -56,48 +56,60 @@
 #endif
 
 /* Head bits G (the guess of a region's entering state starts at the root G
- * bits before it): whole bytes, on the code-length lattice (a multiple of
- * the gcd of the code lengths: a chain started off it never meets the true
- * one), at most HH_FSM_GMAX and the region bits S; none for a fixed-length code (regions start
- * on its lattice, where the root is always right).  On kjv a 64-bit head
- * leaves 6.7 % of the guesses wrong, a 128-bit head 0.3 %: a wave walks
- * only in 15 % of its tiles. */
-HH_FD uint32_t hh_fsm_pick_head(const hh_tables *t, uint32_t S) {
+ * bits before it): whole count steps (cb bits), on the code-length lattice
+ * (a multiple of the gcd of the code lengths: a chain started off it never
+ * meets the true one), at most HH_FSM_GMAX and the region bits S; none for
+ * a fixed-length code (regions start on its lattice, where the root is
+ * always right).  On kjv a 64-bit head leaves 6.7 % of the guesses wrong, a
+ * 128-bit head 0.3 %: a wave walks only in 15 % of its tiles. */
+HH_FD uint32_t hh_fsm_pick_head(const hh_tables *t, uint32_t S, uint32_t cb) {
     if (t->fixed_len > 0) return 0u;
     const uint32_t g = t->len_gcd > 0 ? (uint32_t)t->len_gcd : 1u;
-    uint32_t a = 8, b = g;
+    uint32_t a = cb, b = g;
     while (b) { const uint32_t x = a % b; a = b; b = x; }
-    const uint32_t l = 8 / a * g;                  /* lcm(8, g) */
+    const uint32_t l = cb / a * g;                 /* lcm(cb, g) */
     const uint32_t gmax = S < HH_FSM_GMAX ? S : HH_FSM_GMAX;   /* (within the region before) */
     return l > gmax ? 0u : gmax / l * l;
 }
 
+/* Region bits of the state machine for a tree of ns states whose code
+ * lengths share the gcd g: S_default (the byte-stepped default) for ns <=
+ * HH_FSM_MAXS8; HH_FSM_S7 (7-bit count steps) for larger trees, when it is
+ * on the code lattice; 0: none. */
+HH_FD uint32_t hh_fsm_region_bits(uint32_t ns, uint32_t g, uint32_t S_default) {
+    if (ns <= HH_FSM_MAXS8) return S_default;
+    if (ns > HH_FSM_MAXS) return 0u;
+    return g == 0 || HH_FSM_S7 % g == 0 ? HH_FSM_S7 : 0u;
+}
+
 typedef struct {
-    const uint16_t *ct;      /* 8-bit steps: next << 9 | completed */
+    const uint16_t *ct;      /* cb-bit steps: next << (cb + 1) | completed */
     const uint32_t *b1;      /* 1-bit steps: next | completed << 8 | sym << 16 */
     const uint8_t *tsym;     /* tail-rule symbol of a state */
+    uint32_t cb;             /* count step bits (8 or 7) */
 } hh_fsm_view;
 
-/* stream bit p's byte-aligned 8 bits (p % 8 == 0) / single bit */
-HH_FD uint32_t fsm_byte(const uint32_t *w, uint64_t p) { return (w[p >> 5] >> (p & 31)) & 255u; }
+/* stream bits [p, p + n), n <= 25, p + n <= the readable bits (the word
+ * after p's is read only when the bits reach into it) / a single bit */
+HH_FD uint32_t fsm_win(const uint32_t *w, uint64_t p, uint32_t n) {
+    const uint32_t o = (uint32_t)(p & 31), lo = w[p >> 5] >> o;
+    const uint32_t v = o + n > 32 ? lo | (w[(p >> 5) + 1] << (32 - o)) : lo;
+    return v & ((1u << n) - 1u);
+}
 HH_FD uint32_t fsm_bit(const uint32_t *w, uint64_t p) { return (w[p >> 5] >> (p & 31)) & 1u; }
 
-/* The state machine from state s over stream bits [p, e): whole bytes while
- * p is byte aligned, then single bits.  *n += the codes completed. */
+/* The state machine from state s over stream bits [p, e): whole count steps
+ * (cb bits, at any position: a step's result does not depend on where codes
+ * start), then single bits.  *n += the codes completed. */
 HH_FD uint32_t fsm_run(const hh_fsm_view *F, const uint32_t *w, uint64_t p, uint64_t e, uint32_t s,
                        uint32_t *n) {
     uint32_t c = 0;
-    while (p < e && (p & 7)) {
-        const uint32_t v = F->b1[s * 2 + fsm_bit(w, p)];
-        s = v & 255u;
-        c += (v >> 8) & 255u;
-        p++;
-    }
-    while (p + 8 <= e) {
-        const uint32_t v = F->ct[s * 256 + fsm_byte(w, p)];
-        s = HH_FSM_CT_NEXT(v);
+    const uint32_t cb = F->cb;
+    while (p + cb <= e) {
+        const uint32_t v = F->ct[(s << cb) | fsm_win(w, p, cb)];
+        s = HH_FSM_CT_NEXT(v, cb);
         c += HH_FSM_CT_CNT(v);
-        p += 8;
+        p += cb;
     }
     while (p < e) {
         const uint32_t v = F->b1[s * 2 + fsm_bit(w, p)];
@@ -123,26 +135,27 @@ HH_FD uint32_t fsm_region(const hh_fsm_view *F, const uint32_t *w, uint64_t R, u
 }
 
 /* Two chains in states *A and *B over the region [R, Re) (capped by the
- * stream end): stepped together, a byte at a time (a bit at a time past the
- * last whole byte), until they are in the same state at the same position.
- * Returns 1 if they met; *d += (A's codes - B's codes) up to there, or over
- * the whole region (tail rule included) if they did not. */
+ * stream end): stepped together, a count step at a time (a bit at a time
+ * past the last whole step), until they are in the same state at the same
+ * position.  Returns 1 if they met; *d += (A's codes - B's codes) up to
+ * there, or over the whole region (tail rule included) if they did not. */
 HH_FD int fsm_walk2(const hh_fsm_view *F, const uint32_t *w, uint64_t R, uint64_t Re, uint64_t bits,
                     uint32_t *A, uint32_t *B, int32_t *d) {
     const uint64_t e = Re < bits ? Re : bits;
+    const uint32_t cb = F->cb;
     uint32_t a = *A, b = *B;
     int32_t dd = 0;
     uint64_t p = R;
     while (p < e && a != b) {
         uint32_t va, vb;
-        if (!(p & 7) && p + 8 <= e) {
-            const uint32_t x = fsm_byte(w, p);
-            va = F->ct[a * 256 + x];
-            vb = F->ct[b * 256 + x];
-            p += 8;
+        if (p + cb <= e) {
+            const uint32_t x = fsm_win(w, p, cb);
+            va = F->ct[(a << cb) | x];
+            vb = F->ct[(b << cb) | x];
+            p += cb;
             dd += (int32_t)HH_FSM_CT_CNT(va) - (int32_t)HH_FSM_CT_CNT(vb);
-            a = HH_FSM_CT_NEXT(va);
-            b = HH_FSM_CT_NEXT(vb);
+            a = HH_FSM_CT_NEXT(va, cb);
+            b = HH_FSM_CT_NEXT(vb, cb);
             continue;
         } else {
             const uint32_t x = fsm_bit(w, p);

@@ -13,13 +13,13 @@
 // launch shapes that go with them.
 struct FsmDev {
     uint32_t ok;             // tables built and uploaded
-    uint32_t ns, K, r, S, G;
+    uint32_t ns, K, r, S, G, cb;   // cb: count step bits (8, or 7 for trees of > 127 states)
     uint16_t *ct;
     uint32_t *b1;
     uint8_t *tsym;
     uint64_t *et, *er;
     // persistent grids (workgroups), sized by the occupancy API for S / ns
-    uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K, sized_sco;
+    uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K, sized_sco, sized_cb;
     uint32_t sco;            // k_emf's static copy-out (every tile output <= 16 KiB by the tree)
     uint64_t *dbg;           // HH_DIAG builds: phase cycles of k_cnt (16 x u64, the decoder's)
 };
@@ -29,8 +29,10 @@ struct FsmDev {
 // in_state.  Outputs: *total symbols written to d_out, *leave (state after
 // the last tile), *entry (state entering tile emit_from).  ms[0..2]: count,
 // scan, emission device time.  Returns HH_OK, HH_ERR_CAPACITY, HH_ERR_DEVICE,
-// HH_ERR_NOMEM or HH_ERR_UNSUPPORTED (chains that did not meet within
-// HH_FSM_KM regions: a code that does not resynchronise).
+// HH_ERR_NOMEM, HH_ERR_UNSUPPORTED (no tables) or the internal HH_NOSYNC
+// (chains that did not meet within HH_FSM_KM regions: a code that does not
+// resynchronise; never returned through the C ABI -- the callers take the
+// segment path or report HH_ERR_UNSUPPORTED).
 struct FsmWs {
     void *p;
     size_t size;

@@ -447,6 +447,13 @@ static uint32_t fsm_walk(const hh_tables *T, uint32_t node, uint32_t v, unsigned
     return node;
 }
 
+uint32_t hh_fsm_nstates(const void *tv) {
+    const hh_tables *T = (const hh_tables *)tv;
+    uint32_t ns = 0;
+    for (uint32_t i = 0; i < T->tree_used; i++) ns += !tleaf(T, i);
+    return ns;
+}
+
 int hh_fsm_build(const void *tv, uint32_t S, uint32_t Kreq, hh_fsm_tables *F) {
     const hh_tables *T = (const hh_tables *)tv;
     /* states: the internal nodes, in compact (BFS) order, root = 0 */
@@ -464,19 +471,27 @@ int hh_fsm_build(const void *tv, uint32_t S, uint32_t Kreq, hh_fsm_tables *F) {
         }
     }
     if (ns == 0 || st[0] != 0) { rc = HH_ERR_UNSUPPORTED; goto out; }
-    memset(F, 0, sizeof(*F));
-    F->ns = ns;
     if (Kreq != 0 && Kreq != 6 && Kreq != 7) { rc = HH_ERR_ARG; goto out; }
-    F->K = T->minlen >= 2 ? (Kreq ? Kreq : 6u) : 4u;
-    F->S = S;
-    F->r = S % F->K;
+    {
+        /* the count step: a 16-bit entry holds the next row (state << (CB + 1)) */
+        const uint32_t cb = ns <= HH_FSM_MAXS8 && S % 8 == 0 ? 8u : 7u;
+        if (S == 0 || S % cb) { rc = HH_ERR_UNSUPPORTED; goto out; }
+        memset(F, 0, sizeof(*F));
+        F->ns = ns;
+        F->cb = cb;
+        F->K = T->minlen >= 2 ? (Kreq ? Kreq : 6u) : 4u;
+        if (ns > HH_FSM_MAXS8 && F->K == 7) F->K = 6;   /* (the et row field is 17 bits) */
+        F->S = S;
+        F->r = S % F->K;
+    }
     for (uint32_t s = 0; s < ns; s++) {
         const uint32_t nd = node[s];
+        const uint32_t cb = F->cb;
         F->tsym[s] = T->tsym[nd];
         uint32_t sy, n;
-        for (uint32_t v = 0; v < 256; v++) {
-            const uint32_t to = fsm_walk(T, nd, v, 8, 0, &sy, &n);
-            F->ct[s * 256 + v] = (uint16_t)(((uint32_t)st[to] << 9) | n);
+        for (uint32_t v = 0; v < (1u << cb); v++) {
+            const uint32_t to = fsm_walk(T, nd, v, cb, 0, &sy, &n);
+            F->ct[(s << cb) | v] = (uint16_t)(((uint32_t)st[to] << (cb + 1)) | n);
         }
         for (uint32_t bit = 0; bit < 2; bit++) {
             const uint32_t to = fsm_walk(T, nd, bit, 1, 1, &sy, &n);

@@ -278,13 +278,19 @@ def iid_stream(hf, text: np.ndarray, target_bytes: int, device="cuda", seed: int
                chunk: int = 1 << 27) -> IIDStream:
     """The i.i.d. stream cut at the last whole symbol within target_bytes of
     payload, encoded on the GPU with hf's codebook."""
+    return iid_stream_from(hf.tree(), unigram_cum(text), target_bytes, device, seed, chunk)
+
+
+def iid_stream_from(tree, cum: np.ndarray, target_bytes: int, device="cuda", seed: int = IID_SEED,
+                    chunk: int = 1 << 27) -> IIDStream:
+    """i.i.d. symbols with the cumulative counts cum (int64[256], splitmix64
+    seed `seed`), cut at the last whole symbol within target_bytes of
+    payload, encoded on the GPU with tree's codes."""
     import torch
-    tree = hf.tree()
-    code, lens = code_table(tree)
-    cum = unigram_cum(text)
+    code, lens = code_table(tree, 60)
     T = int(cum[-1])
     cum_t = torch.as_tensor(cum, device=device)
-    p = np.bincount(text, minlength=256) / T
+    p = np.diff(np.concatenate([[0], cum])) / T
     n = int(8 * target_bytes / float((p * lens).sum()) * 1.01) + 64    # a little more than fits
     syms = torch.empty(n, dtype=torch.uint8, device=device)
     for c0 in range(0, n, chunk):
@@ -306,3 +312,58 @@ def iid_stream(hf, text: np.ndarray, target_bytes: int, device="cuda", seed: int
     syms = syms[:keep].clone()
     payload, bits = encode_gpu(syms, code, lens, device, chunk)
     return IIDStream(tree, payload, bits, syms)
+
+
+# ---------------------------------------------------------------------------
+# Byte-alphabet stream: a Huffman code over all 256 byte values (255
+# internal nodes, the largest tree a byte alphabet gives -- the state
+# machine's 7-bit count steps) for i.i.d. bytes with Zipf-like frequencies.
+# ---------------------------------------------------------------------------
+BYTE_SEED = 0xB17E5EED
+ZIPF_S = 1.1
+
+
+def byte_counts(seed: int = BYTE_SEED, s: float = ZIPF_S) -> np.ndarray:
+    """Counts of the 256 byte values: 2^20 / rank^s (+1), ranks a seeded
+    permutation (int64[256], every value present)."""
+    rank = np.random.default_rng(seed).permutation(256) + 1
+    return (np.floor(float(1 << 20) / rank.astype(np.float64) ** s) + 1).astype(np.int64)
+
+
+def huffman_tree(counts: np.ndarray):
+    """A Huffman code for the symbols with counts > 0, in the reference's
+    layout (huffdata.h:12-16: node 0 the root, pre-order, leaves
+    izero = ione = -1): deterministic (ties broken by insertion order)."""
+    import heapq
+    from huffmandecoderongpus_amd import Tree
+    heap = [(int(c), i, ("leaf", i)) for i, c in enumerate(counts) if c > 0]
+    heapq.heapify(heap)
+    k = len(heap)
+    if k == 1:
+        heap = [(heap[0][0], 0, ("node", heap[0][2], ("leaf", (heap[0][2][1] + 1) & 255)))]
+    while len(heap) > 1:
+        a = heapq.heappop(heap)
+        b = heapq.heappop(heap)
+        heapq.heappush(heap, (a[0] + b[0], k, ("node", a[2], b[2])))
+        k += 1
+    iz, io, sy = [], [], []
+
+    def emit(t):
+        v = len(iz)
+        iz.append(-1); io.append(-1); sy.append(0)
+        if t[0] == "leaf":
+            sy[v] = t[1]
+        else:
+            iz[v] = emit(t[1])
+            io[v] = emit(t[2])
+        return v
+    emit(heap[0][2])
+    return Tree(np.array(iz, np.int32), np.array(io, np.int32), np.array(sy, np.uint8))
+
+
+def byte_stream(target_bytes: int, device="cuda", seed: int = BYTE_SEED, chunk: int = 1 << 27) -> IIDStream:
+    """i.i.d. bytes with byte_counts(seed) frequencies, Huffman-coded
+    (huffman_tree), cut within target_bytes of payload, encoded on the GPU."""
+    counts = byte_counts(seed)
+    return iid_stream_from(huffman_tree(counts), np.cumsum(counts).astype(np.int64), target_bytes, device,
+                           seed, chunk)

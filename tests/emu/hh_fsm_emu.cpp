@@ -44,18 +44,20 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
     int rc = hh_tables_build(&tree, &g_T);
     if (rc) return rc;
     for (int i = 0; i < 9; i++) stats[i] = 0;
-    if (S == 0) S = hh_pick_region_bits((uint32_t)g_T.len_gcd);
+    if (S == 0)
+        S = hh_fsm_region_bits(hh_fsm_nstates(&g_T), (uint32_t)g_T.len_gcd,
+                               hh_pick_region_bits((uint32_t)g_T.len_gcd));
     if (S < 32 || S % 32) return HH_ERR_ARG;
     rc = hh_fsm_build(&g_T, S, g_K, &g_F);
     if (rc) return rc;
-    uint32_t G = G_req >= 0 ? (uint32_t)G_req : hh_fsm_pick_head(&g_T, S);
-    if (G % 8 || G > HH_FSM_GMAX || G > S) return HH_ERR_ARG;
+    uint32_t G = G_req >= 0 ? (uint32_t)G_req : hh_fsm_pick_head(&g_T, S, g_F.cb);
+    if (G % g_F.cb || G > HH_FSM_GMAX || G > S) return HH_ERR_ARG;
     stats[3] = S;
     stats[4] = G;
     if (leave) *leave = in_state;
     if (entry) *entry = in_state;
     if (bits == 0) return 0;
-    const hh_fsm_view F = {g_F.ct, g_F.b1, g_F.tsym};
+    const hh_fsm_view F = {g_F.ct, g_F.b1, g_F.tsym, g_F.cb};
     const uint64_t nw = (bits + 7) / 8 / 4 + 24;
     std::vector<uint32_t> wv(nw, 0u);
     memcpy(wv.data(), data, (bits + 7) / 8);
@@ -145,7 +147,7 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
     // scan (prologue tiles emit nothing) and emission
     uint64_t o = 0;
     const uint32_t K = g_F.K, r = g_F.r;
-    uint8_t buf[4096];
+    uint8_t buf[8192];
     for (uint64_t t = prologue; t < nt; t++) {
         const uint64_t T0 = t * TB;
         for (int j = 0; j < NR; j++) {
@@ -214,12 +216,16 @@ int64_t hh_fsm_emu_tables(const int32_t *izero, const int32_t *ione, const uint8
     hh_tree tree = {nodes, izero, ione, sym};
     int rc = hh_tables_build(&tree, &g_T);
     if (rc) return rc;
+    if (S == 0)
+        S = hh_fsm_region_bits(hh_fsm_nstates(&g_T), (uint32_t)g_T.len_gcd,
+                               hh_pick_region_bits((uint32_t)g_T.len_gcd));
     rc = hh_fsm_build(&g_T, S, g_K, &g_F);
     if (rc) return rc;
     info[0] = g_F.ns;
     info[1] = g_F.K;
     info[2] = g_F.r;
-    info[3] = hh_fsm_pick_head(&g_T, S);
+    info[3] = hh_fsm_pick_head(&g_T, S, g_F.cb);
+    info[4] = g_F.cb;
     return HH_OK;
 }
 

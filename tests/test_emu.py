@@ -325,17 +325,55 @@ def test_fsm_tables_shape(femu):
     """State machine sizes of the fixtures: emission steps of 6 bits for codes
     of >= 2 bits, a 4-bit remainder step for 256-bit regions."""
     hf = H.HuffFile.load(os.path.join(FILES, "kjv.txt.huff"))
-    info = np.zeros(4, np.uint32)
+    info = np.zeros(5, np.uint32)
     iz = np.ascontiguousarray(hf.izero, np.int32)
     io = np.ascontiguousarray(hf.ione, np.int32)
     sy = np.ascontiguousarray(hf.sym, np.uint8)
     assert femu.hh_fsm_emu_tables(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), 256,
                                   info.ctypes.data) == 0
-    assert list(info) == [83, 6, 4, 128]
+    assert list(info) == [83, 6, 4, 128, 8]
     femu.hh_fsm_emu_set_k(7)
     try:
         assert femu.hh_fsm_emu_tables(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), 256,
                                       info.ctypes.data) == 0
     finally:
         femu.hh_fsm_emu_set_k(0)
-    assert list(info) == [83, 7, 4, 128]
+    assert list(info) == [83, 7, 4, 128, 8]
+    # a byte alphabet (256 leaves, 255 states): 7-bit count steps over
+    # 224-bit regions (an entry's 16 bits hold an 8-bit state's row), 6-bit
+    # emission steps whatever is asked (the et row field), 126-bit heads
+    rng = np.random.default_rng(5)
+    iz, io, sy, _ = random_tree(rng, 256)
+    iz, io, sy = (np.ascontiguousarray(a, t) for a, t in ((iz, np.int32), (io, np.int32), (sy, np.uint8)))
+    for K in (0, 7):
+        femu.hh_fsm_emu_set_k(K)
+        try:
+            assert femu.hh_fsm_emu_tables(iz.ctypes.data, io.ctypes.data, sy.ctypes.data, len(iz), 0,
+                                          info.ctypes.data) == 0
+        finally:
+            femu.hh_fsm_emu_set_k(0)
+        assert list(info) == [255, 6, 224 % 6, 126, 7]
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_fsm_byte_alphabet_trees(femu, seed):
+    """Trees of 129..256 leaves (128..255 states, more than 8-bit count steps
+    can number): 7-bit count steps over 224-bit regions, streams cut inside
+    codes (tail rule), 6- and 7-bit emission asked for, against the
+    oracle."""
+    rng = np.random.default_rng(1000 + seed)
+    nleaves = int(rng.integers(129, 257))
+    iz, io, sy, syms = random_tree(rng, nleaves)
+    t = H.Tree(iz, io, sy)
+    if t.info()["maxlen"] > 64:
+        pytest.skip("encoder limit")
+    p = rng.dirichlet(np.full(nleaves, 0.3))
+    text = rng.choice(syms, size=int(rng.integers(30000, 120000)), p=p).astype(np.uint8)
+    data, bits = t.encode(text)
+    for cut in (bits, bits - 1, max(1, bits // 3 + 1), 14336 * 2 + 5):
+        cut = min(cut, bits)
+        ref = oracle_chain(iz, io, sy, data, cut)
+        for K in (0, 7):
+            n, out, st, _, _ = run_femu(femu, iz, io, sy, data, cut, K=K)
+            assert st[3] == 224 and st[4] % 7 == 0, st
+            assert n == len(ref) and np.array_equal(out, ref), (cut, K, st)

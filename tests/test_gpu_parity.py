@@ -285,30 +285,148 @@ def test_evaluate_scope_pipeline(hh, files_dir, chunk_kb, mib, monkeypatch):
                                  {"HH_FRONT_WALK": "8192"}, {"HH_EMIT_XPT": "0"},
                                  {"HH_EMIT_XPT": "1"}, {"HH_EMIT_NW": "8"}])
 def test_walk_bound_and_deferral_lists(hh, files_dir, env, monkeypatch):
-    """The work the fast path moves out of its waves -- walks longer than
-    the front's bound (to k_walk), runs over several regions (to k_emitx,
-    through per-wave lists that may fill up) -- must give the same bytes
-    whichever part of it moves: every walk in k_front (8192), a few, none
-    (0, the default); no run deferred (0), lists that overflow (1); k_emit's
-    8-wave workgroups (taken when a tree's tables leave no room for 16)."""
+    """Round 2's pipeline (HH_FLAG_LEGACY: k_front -> k_walk -> k_table ->
+    k_scan -> k_emit -> k_emitx) moves work out of its waves -- walks longer
+    than the front's bound (to k_walk), runs over several regions (to
+    k_emitx, through per-wave lists that may fill up) -- and must give the
+    same bytes whichever part of it moves: every walk in k_front (8192), a
+    few, none (0, the default); no run deferred (0), lists that overflow
+    (1); k_emit's 8-wave workgroups.  The knobs are read only by that
+    pipeline, so the decoder is built with FLAG_LEGACY and the test asserts
+    that pipeline (not the state machine) ran."""
     import torch
     from huffmandecoderongpus_amd import synth
     for k, v in env.items():
         monkeypatch.setenv(k, v)                # read when the tree is set
     hf, text = synth.load_source(files_dir, "kjv.txt")
     syn = synth.tiled_stream(hf, text, 64 << 20)
-    dec = hh.Decoder(0)
+    dec = hh.Decoder(0, flags=hh.FLAG_LEGACY)
     try:
         dec.set_tree(syn.tree)
         out = torch.full((syn.decoded_bytes + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
         n = dec.decode_device(syn.data, syn.bits, out)
         torch.cuda.synchronize()
+        st = dec.stats()
+        assert st["state_machine"] == 0 and st["exact_fallback"] == 0 and st["fixed_length"] == 0, st
         assert n == syn.decoded_bytes
         assert synth.verify_tiled(out, syn)
         assert int(out[n:n + 64].ne(0xAB).sum()) == 0
-        assert dec.stats()["exact_fallback"] == 0
     finally:
         dec.close()
+
+
+@pytest.mark.parametrize("name", FIXTURES)
+def test_fixture_legacy_pipeline(hh, files_dir, name):
+    """Every fixture through round 2's pipeline (HH_FLAG_LEGACY), device
+    side, byte-exact -- the path trees the state machine does not take fall
+    back to."""
+    import torch
+    path = os.path.join(files_dir, name + ".huff")
+    hf = hh.HuffFile.load(path)
+    ref = O.OracleHuff.load(path).chain_decode()
+    dec = hh.Decoder(0, flags=hh.FLAG_LEGACY | hh.FLAG_NO_FIXED)
+    try:
+        dec.set_tree(hf.tree())
+        d_in = torch.from_numpy(hf.data.copy()).cuda()
+        d_out = torch.zeros(hf.uncompressedsize + 64, dtype=torch.uint8, device="cuda")
+        n = dec.decode_device(d_in, hf.bits, d_out)
+        torch.cuda.synchronize()
+        st = dec.stats()
+        assert st["state_machine"] == 0 and st["fixed_length"] == 0 and st["exact_fallback"] == 0, st
+        assert n == len(ref)
+        assert np.array_equal(d_out[:n].cpu().numpy(), ref)
+        assert int(d_out[n:].sum().item()) == 0
+    finally:
+        dec.close()
+
+
+def _byte_alphabet_stream(hh, seed, nleaves, nbytes):
+    """A natural variable-length code over a byte alphabet: a random tree of
+    `nleaves` leaves (nleaves - 1 internal nodes) and i.i.d. symbols from a
+    Dirichlet(0.3) distribution over them, encoded by the host encoder to
+    about `nbytes` of payload."""
+    rng = np.random.default_rng(seed)
+    iz, io, sy, syms = _random_tree(rng, nleaves)
+    t = hh.Tree(iz, io, sy)
+    p = rng.dirichlet(np.full(nleaves, 0.3))
+    info = t.info()
+    # expected bits per symbol from a sample, to size the text
+    probe = rng.choice(syms, size=20000, p=p).astype(np.uint8)
+    _, pb = t.encode(probe)
+    nsym = int(nbytes * 8 / (pb / probe.size))
+    text = rng.choice(syms, size=nsym, p=p).astype(np.uint8)
+    data, bits = t.encode(text)
+    return iz, io, sy, t, info, text, data, bits
+
+
+@pytest.mark.parametrize("seed,nleaves", [(11, 256), (12, 256), (13, 200)])
+def test_byte_alphabet_code(hh, seed, nleaves):
+    """SURVEY 8(a10)'s large trees: a natural variable-length code over 200
+    or 256 symbols (199 / 255 internal nodes: more states than round 3's
+    state machine took) on a >= 64 MiB stream and on cut streams, through the
+    DEFAULT decoder, byte-exact against the oracle's restatement of the
+    reference's serial decode (decodeallbits.cl:10-33 accepts any tree)."""
+    import torch
+    iz, io, sy, t, info, text, data, bits = _byte_alphabet_stream(hh, seed, nleaves, 64 << 20)
+    assert info["leaves"] == nleaves and info["reachable"] == 2 * nleaves - 1
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(t)
+        buf = np.zeros((bits + 7) // 8 + 64, np.uint8)
+        buf[: (bits + 7) // 8] = data[: (bits + 7) // 8]
+        d_in = torch.from_numpy(buf).cuda()
+        d_out = torch.full((text.size + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+        n = dec.decode_device(d_in, bits, d_out)
+        torch.cuda.synchronize()
+        st = dec.stats()
+        assert st["exact_fallback"] == 0 and st["state_machine"] == 1, st
+        assert n == text.size
+        assert torch.equal(d_out[:n], torch.from_numpy(text).cuda())
+        assert int(d_out[n:n + 64].ne(0xAB).sum()) == 0
+        # cut streams (tail rule) against the oracle, on a 4 MiB prefix
+        small = min(bits, 32 << 20)
+        for cut in (small, small - 1, small // 3 + 7, 1000003):
+            ref = _oracle(iz, io, sy, data, cut)
+            got = _decode_dev(hh, dec, data, cut, cut + 16)
+            assert dec.stats()["exact_fallback"] == 0
+            assert len(got) == len(ref) and np.array_equal(got, ref), cut
+        # the whole stream against the oracle too (not only the encoder's input)
+        ref = _oracle(iz, io, sy, data, bits)
+        assert ref.size == text.size and np.array_equal(ref, text)
+    finally:
+        dec.close()
+
+
+@pytest.mark.parametrize("mib", [64, 1024])
+def test_byte_alphabet_huffman_stream(hh, mib):
+    """bench's byte-alphabet workload: a Huffman code over all 256 byte values
+    (255 states: 7-bit count steps, 224-bit regions), i.i.d. Zipf bytes
+    encoded on the GPU; the default decoder must return the symbols, on the
+    state machine; at 64 MiB the payload's first 256 KiB is also checked
+    against the host encoder."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    s = synth.byte_stream(mib << 20)
+    if mib == 64:
+        pay, _ = s.tree.encode(s.syms[: 1 << 20].cpu().numpy())
+        assert np.array_equal(s.data[: 1 << 18].cpu().numpy(), pay[: 1 << 18])
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(s.tree)
+        assert dec.tile_bits() == 64 * 224
+        out = torch.full((s.decoded_bytes + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+        for _ in range(2):
+            n = dec.decode_device(s.data, s.bits, out)
+            torch.cuda.synchronize()
+            st = dec.stats()
+            assert st["state_machine"] == 1 and st["exact_fallback"] == 0, st
+            assert n == s.decoded_bytes
+            assert torch.equal(out[:n], s.syms)
+            assert int(out[n:n + 64].ne(0xAB).sum()) == 0
+    finally:
+        dec.close()
+        del out, s
+        torch.cuda.empty_cache()
 
 
 @pytest.mark.parametrize("mib", [64, 1024])

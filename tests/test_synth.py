@@ -62,3 +62,26 @@ def test_code_table_matches_code_lengths(kjv):
     assert np.array_equal(lens, synth.code_lengths(hf.tree()))
     present = np.nonzero(lens)[0]
     assert len(set((int(code[s]), int(lens[s])) for s in present)) == len(present)
+
+
+def test_byte_alphabet_huffman_tree():
+    """bench's byte-alphabet codebook: a Huffman code over all 256 byte
+    values (255 internal nodes), complete (Kraft sum 1), its mean code
+    length within a bit of the entropy, and an encode -> oracle decode round
+    trip of i.i.d. symbols drawn from its frequencies (host twin of the
+    GPU generator)."""
+    from huffmandecoderongpus_amd import synth
+    counts = synth.byte_counts()
+    assert counts.size == 256 and (counts > 0).all()
+    t = synth.huffman_tree(counts)
+    info = t.info()
+    assert info["leaves"] == 256 and info["reachable"] == 511
+    code, L = synth.code_table(t, 60)
+    assert abs(sum(2.0 ** -int(x) for x in L) - 1.0) < 1e-12
+    p = counts / counts.sum()
+    H_ = float(-(p * np.log2(p)).sum())
+    assert H_ <= float((p * L).sum()) < H_ + 1
+    syms = synth.iid_symbols_np(np.cumsum(counts).astype(np.int64), 0, 200000, synth.BYTE_SEED)
+    data, bits = t.encode(syms)
+    hf = O.Huff(bits, 0, t.izero, t.ione, t.sym, data[: (bits + 7) // 8])
+    assert np.array_equal(O.OracleHuff.from_arrays(hf).chain_decode(), syms)
