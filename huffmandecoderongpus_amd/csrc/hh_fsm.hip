@@ -52,6 +52,9 @@
 #define HH_CNT_PNX 0          // k_cnt walks: region j+1's words prefetched a tile ahead (1) or loaded at
                               // a walk (0); reading them from lane j+1 measured no faster
 #endif
+#ifndef HH_CNT_IL
+#define HH_CNT_IL 0           // k_cnt: the next tile's heads interleaved with this tile's counts (measured no faster)
+#endif
 #ifndef HH_WALK_MASK
 #define HH_WALK_MASK 1        // k_cnt walks: only the lanes not met yet look up
 #endif
@@ -221,10 +224,19 @@ template <uint32_t CB>
 struct CntFmt {
     static constexpr uint32_t RS = CB + 1;                          // row = state << RS
     static constexpr uint32_t RM = CB == 8 ? 0xfe00u : 0xff00u;     // the row bits of an entry
+    // the counts of a sum of entries: bits 4 .. RS - 1 of an entry (between
+    // its count and its row) are 0, so the low RS bits of a sum of entries
+    // are the sum of their counts while that is below 2^RS (a region's count
+    // steps complete at most S < 2^RS codes)
+    static constexpr uint32_t CM = (1u << RS) - 1u;
 };
+// (the kernels using the count table declare no static LDS: the dynamic
+// LDS, and with it the table, starts at address 0, and the lookup address
+// is the AND-OR alone -- v_and_or_b32, no base add)
+typedef const uint16_t __attribute__((address_space(3))) *lds_u16p;
 template <uint32_t CB>
-__device__ __forceinline__ uint32_t ct_at(const uint8_t *lds, uint32_t row, uint32_t off) {
-    return *(const uint16_t *)(lds + ((row & CntFmt<CB>::RM) | off));
+__device__ __forceinline__ uint32_t ct_at(const uint8_t *, uint32_t row, uint32_t off) {
+    return *(lds_u16p)(uintptr_t)((row & CntFmt<CB>::RM) | off);
 }
 // step k's table offset (its CB bits << 1) in a region held in registers
 template <uint32_t SW, uint32_t CB>
@@ -251,22 +263,53 @@ __device__ __noinline__ int cnt_fix_next(const hh_fsm_view *F, const uint32_t *w
 // region's readable bits (S unless the stream ends inside it); only the TAIL
 // instantiations check it.
 // ---------------------------------------------------------------------------
-template <uint32_t SW, bool TAIL, uint32_t CB>
+// Head steps: the last HS count steps of a region (at most HH_FSM_GMAX bits);
+// a head reads the region's words from HWL on.
+template <uint32_t SW, uint32_t CB>
+struct HeadGeo {
+    static constexpr uint32_t S = 32 * SW, NS = S / CB;
+    static constexpr uint32_t HS = NS < HH_FSM_GMAX / CB ? NS : HH_FSM_GMAX / CB;
+    static constexpr uint32_t HWL = (S - CB * HS) / 32;
+};
+
+// The count chain of region j from state s.  IL: the NEXT tile's head chain
+// (*hg, from the root over the last HS steps of region j of that tile -- the
+// full head, G = CB * HS -- words wn) runs interleaved with it, head step h
+// after count step h * NS / HS: two independent chains of LDS lookups in
+// flight instead of one.
+template <uint32_t SW, bool TAIL, uint32_t CB, bool IL = false>
 __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
-                                               uint32_t s, uint32_t lim, uint32_t *n) {
-    uint32_t c = 0;
+                                               uint32_t s, uint32_t lim, uint32_t *n, const uint32_t *wn = nullptr,
+                                               uint32_t *hg = nullptr) {
+    typedef HeadGeo<SW, CB> HG;
+    uint32_t c = 0, h = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 32 * SW / CB; k++) {
         if (!TAIL || CB * k + CB <= lim) {
             const uint32_t e = ct_at<CB>(lds, s, cstep<SW, CB>(w, k));
             s = e;
-            c += e & 15u;
-            // (the count added at its step: left to the scheduler, the adds
+            c += e;                              // (the counts: c's low RS bits, CntFmt::CM)
+            // (the entry added at its step: left to the scheduler, the adds
             // sink to the end of the chain and every step's entry stays live
             // -- 32 registers, the difference between 24 and 32 waves per CU)
             asm volatile("" : "+v"(c));
         }
+        if (IL) {
+#pragma unroll
+            for (uint32_t i = 0; i < HG::HS; i++)
+                if (i * HG::NS / HG::HS == k) {
+                    const uint32_t q = HG::NS - HG::HS + i;      // (the head's step index in its region)
+                    // (IL: G = CB * HS, the full head.  The step's offset
+                    // opaque: merged into the address, it costs 4 VALU
+                    // instead of an extract and an AND-OR)
+                    uint32_t o = cstep<SW, CB>(wn, q);
+                    asm volatile("" : "+v"(o));
+                    h = ct_at<CB>(lds, h, o);
+                }
+        }
     }
+    if (IL) *hg = h & CntFmt<CB>::RM;
+    c &= CntFmt<CB>::CM;
     s &= CntFmt<CB>::RM;
     if (TAIL)
         for (uint32_t q = lim / CB * CB; q < lim; q++) s = b1_row<CB>(b1, s, rbit_dyn<SW>(w, q), &c);   // the last partial step
@@ -334,11 +377,51 @@ __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns, uint32_t cb) {
 // here from pv, the 16 bytes before the tile).  Returns lane 63's head (the
 // next tile's region-0 guess), as a row.
 #define HIN_NONE 0xffffffffu
-template <uint32_t SW, bool TAIL, uint32_t CB>
+// decodeallbits: lane j's guess gs for region j+1's entering state (a chain
+// from the root over the last G bits of region j) and (hin == HIN_NONE) lane
+// 0's guess hp for its own region 0: the same head over the previous
+// region's last G bits -- pv, the HB bytes before the tile: uniform words, a
+// chain every lane runs alike (broadcast reads), interleaved with its own
+// head.  Both as rows; hp = hin when given.
+template <uint32_t SW, uint32_t CB>
+__device__ __forceinline__ void cnt_heads(const uint8_t *lds, const uint32_t *w, const uint32_t *pv, uint32_t G,
+                                          uint32_t hin, uint32_t &gs, uint32_t &hp) {
+    constexpr uint32_t S = 32 * SW, RM = CntFmt<CB>::RM;
+    constexpr uint32_t NS = S / CB;
+    constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
+    constexpr uint32_t HS = HeadGeo<SW, CB>::HS;   // head steps at most
+    static_assert(HB % 4 == 0, "head bytes in whole words");
+    static_assert(CB * HS <= 8 * HB, "the head of region 0 within the bytes before the tile");
+    const uint32_t GS = G / CB;                       // (uniform)
+    gs = 0;
+    hp = 0;
+    if (hin == HIN_NONE) {
+#pragma unroll
+        for (uint32_t k = NS - HS; k < NS; k++)
+            if (k >= NS - GS) {
+                gs = ct_at<CB>(lds, gs, cstep<SW, CB>(w, k));
+                hp = ct_at<CB>(lds, hp, CB == 8 ? __builtin_amdgcn_ubfe(pv[(k - (NS - HS)) >> 2], 8 * ((k - (NS - HS)) & 3), 8) << 1
+                                                : winsh<HB / 4, CB, 1>(pv, 8 * HB + CB * k - S));
+            }
+        hp &= RM;
+    } else {
+#pragma unroll
+        for (uint32_t k = NS - HS; k < NS; k++)
+            if (k >= NS - GS) gs = ct_at<CB>(lds, gs, cstep<SW, CB>(w, k));
+        hp = hin;
+    }
+    gs &= RM;
+}
+// IL: the heads of this tile are given (gs_il: lane j's guess for region
+// j+1, hin lane 0's for region 0 -- computed while the previous tile was
+// counted), and the next tile's heads are computed here, interleaved with
+// this tile's count, from its words wn -> *gsn.
+template <uint32_t SW, bool TAIL, uint32_t CB, bool IL = false>
 __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
                                              const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
-                                             const uint32_t *nx, const uint32_t *pv, uint32_t hin CDIAG_ARGS) {
-    constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS, RM = CntFmt<CB>::RM;
+                                             const uint32_t *nx, const uint32_t *pv, uint32_t hin CDIAG_ARGS,
+                                             uint32_t gs_il = 0, const uint32_t *wn = nullptr, uint32_t *gsn = nullptr) {
+    constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS;
     const uint32_t j = threadIdx.x & 63u;
     const uint64_t TB = (uint64_t)NR * S, T0 = t * TB;
     const uint64_t R = T0 + (uint64_t)j * S;
@@ -356,42 +439,17 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
 #ifndef HH_XP_NOHEAD
 #define HH_XP_NOHEAD 0        // (timing experiments only: results are wrong)
 #endif
-    if (geo.G && !HH_XP_NOHEAD) {
-        // and lane 0's guess for its own region 0 (tile t > 0): the same head
-        // over the previous region's last G bits -- uniform words (scalar
-        // loads), a chain every lane runs alike (broadcast reads), interleaved
-        // with its own head
-        // head steps: the last G / CB count steps of the region; pv holds
-        // the HB bytes before the tile (lane 0's head reads the same step
-        // positions in them)
-        constexpr uint32_t NS = S / CB;
-        constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
-        constexpr uint32_t HS = NS < HH_FSM_GMAX / CB ? NS : HH_FSM_GMAX / CB;   // head steps at most
-        static_assert(HB % 4 == 0, "head bytes in whole words");
-        static_assert(CB * HS <= 8 * HB, "the head of region 0 within the bytes before the tile");
-        const uint32_t GS = geo.G / CB;                   // (uniform)
-        if (hin == HIN_NONE) {
-#pragma unroll
-            for (uint32_t k = NS - HS; k < NS; k++)
-                if (k >= NS - GS) {
-                    gs = ct_at<CB>(lds, gs, cstep<SW, CB>(w, k));
-                    hp = ct_at<CB>(lds, hp, CB == 8 ? __builtin_amdgcn_ubfe(pv[(k - (NS - HS)) >> 2], 8 * ((k - (NS - HS)) & 3), 8) << 1
-                                                    : winsh<HB / 4, CB, 1>(pv, 8 * HB + CB * k - S));
-                }
-            hp &= RM;
-        } else {
-#pragma unroll
-            for (uint32_t k = NS - HS; k < NS; k++)
-                if (k >= NS - GS) gs = ct_at<CB>(lds, gs, cstep<SW, CB>(w, k));
-            hp = hin;
-        }
-        gs &= RM;
+    if (IL) {
+        gs = gs_il;
+        hp = hin;
+    } else if (geo.G && !HH_XP_NOHEAD) {
+        cnt_heads<SW, CB>(lds, w, pv, geo.G, hin, gs, hp);
     }
     CDIAG_STAMP(0);
     const uint32_t gup = shfl_up1(gs);              // (cross-lane ops with every lane active)
     const uint32_t sp = j ? gup : (t == 0 ? geo.in_state << RS : hp);
     uint32_t n;
-    uint32_t X = cnt_region<SW, TAIL, CB>(lds, F.b1, w, sp, lim, &n);   // region j's exit (given its entry)
+    uint32_t X = cnt_region<SW, TAIL, CB, IL>(lds, F.b1, w, sp, lim, &n, wn, gsn);   // region j's exit (given its entry)
     // the stream ends in region j / in region j+1: the tail rule counts a
     // chain that is not at the root there (fsm_region, fsm_walk2)
     const bool endj = TAIL && lim > 0 && R + lim == geo.bits;
@@ -412,6 +470,7 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
 #define HH_XP_NOWALK 0        // (timing experiments only: results are wrong)
 #endif
     uint32_t nv[SW];
+    bool have_nv = false;
     for (int round = 0; round < (HH_XP_NOWALK ? 0 : NR); round++) {
         const bool want = X != E && limn > 0 && (j < 63 || has_next);
         if (__ballot(want) == 0) break;
@@ -419,12 +478,21 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
         CDIAG_COUNT(2, 1);
         uint32_t A = X, B = want ? E : X;           // (not walking: A == B, no change)
         int32_t dd = 0;
-        if (round == 0) {
-            if (HH_CNT_PNX == 1) {
+        if (HH_CNT_PNX == 1) {
+            if (round == 0) {
 #pragma unroll
                 for (uint32_t k = 0; k < SW; k++) nv[k] = nx[k];
-            } else {
+            }
+        } else {
+            if (round == 0) {
+#pragma unroll
+                for (uint32_t k = 0; k < SW; k++) nv[k] = 0u;
+            }
+            if (want && !have_nv) {
+                // region j+1's words, loaded by the walking lanes only (the
+                // others' lookups are masked off; their words are not used)
                 fs_load<SW>(nv, fs_rsrc(g, uni64(t) * TB / 32, geo.nwords), (j + 1) * SW);
+                have_nv = true;
             }
         }
         // (opaque per round: the byte offsets of the walk are not hoisted out
@@ -545,6 +613,66 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     };
     CDIAG_DECL
     if (t == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
+    if (!TAIL && HH_CNT_IL && !HH_CNT_PNX && geo.G == CB * HeadGeo<SW, CB>::HS) {
+        // Interleaved heads: tile t+1's heads run beside tile t's counts, so
+        // a lane has two independent chains of lookups in flight.  The head
+        // reads a region's words [HWL, SW) only: those of tile t+1 are loaded
+        // two tiles ahead, the rest one tile ahead.
+        constexpr uint32_t HWL = HeadGeo<SW, CB>::HWL;
+        uint32_t wc[SW], wn[SW], wnn[SW];       // (wn, wnn: words [HWL, SW) only; wn's [0, HWL) loaded into wc's)
+        auto load_words = [&](uint32_t *v, uint32_t tt, uint32_t a, uint32_t b) {
+            tt = (uint32_t)__builtin_amdgcn_readfirstlane((int)tt);
+            const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, (uint64_t)tt * TB / 32, geo.nwords);
+            uint32_t ln;
+            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+            if (SW % 4 == 0 && a % 4 == 0 && b % 4 == 0) {
+#pragma unroll
+                for (uint32_t k = 0; k < SW; k += 4)
+                    if (k >= a && k < b) {
+                        const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (ln * SW + k)), 0, 0));
+                        v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
+                    }
+            } else {
+#pragma unroll
+                for (uint32_t k = 0; k < SW; k++)
+                    if (k >= a && k < b) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * (ln * SW + k)), 0, 0);
+            }
+        };
+        if (t < tend) {
+            const uint32_t tn = t + 1 < tend ? t + 1 : t;
+            load_words(wc, t, 0, SW);
+            load_words(wn, tn, HWL, SW);
+            uint32_t pv[HB / 4];
+            {
+                const uint64_t tw = (uint64_t)t * TB / 32, pa = tw >= HB / 4 ? tw - HB / 4 : 0u;   // (tile 0: unused)
+                const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (j % (HB / 4))), 0, 0);
+#pragma unroll
+                for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+            }
+            // the run's first tile: its heads (and lane 0's) on their own
+            uint32_t gs = 0, hp = 0;
+            cnt_heads<SW, CB>(smem, wc, pv, geo.G, HIN_NONE, gs, hp);
+            hp = (uint32_t)__builtin_amdgcn_readfirstlane((int)hp);
+            for (; t < tend; t++) {
+                t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+                const uint32_t tn = t + 1 < tend ? t + 1 : t, tnn = t + 2 < tend ? t + 2 : tn;
+                if (HWL) load_words(wn, tn, 0, HWL);        // tile t+1's words [0, HWL) (its [HWL, SW) arrived)
+                load_words(wnn, tnn, HWL, SW);
+                uint32_t gsn = 0;
+                const uint32_t h63 = cnt_tile<SW, false, CB, true>(smem, F, g, geo, wk, (uint64_t)t, wc, wc, nullptr, hp CDIAG_PASS,
+                                                                   gs, wn, &gsn);
+                hp = (uint32_t)__builtin_amdgcn_readfirstlane((int)h63);
+                gs = gsn;
+#pragma unroll
+                for (uint32_t k = 0; k < SW; k++) {
+                    wc[k] = wn[k];
+                    if (k >= HWL) wn[k] = wnn[k];
+                }
+            }
+        }
+        CDIAG_FLUSH(wk.dbg);
+        return;
+    }
     if (t < tend) prefetch(t);
     uint32_t hin = HIN_NONE;
     for (; t < tend; t += tstep) {
