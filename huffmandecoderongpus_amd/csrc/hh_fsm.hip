@@ -26,9 +26,11 @@
 
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "hh_fsm_algo.h"
 #include "hh_fsm_dev.h"
@@ -69,6 +71,7 @@
 __host__ __device__ constexpr uint32_t emf_waves(uint32_t nch) { return nch == 2 ? HH_EMF2_WAVES : 16u; }
 #define SCAN_TB 1024          // tiles per k_fscan1 block
 #define FX_W 8                // corrections per tile (HH_FSM_KM)
+#define VMCNT0 0x0F70         // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): vector memory only
 static_assert(FX_W == HH_FSM_KM, "corrections per tile");
 
 enum { FF_FAIL = 1, FF_OVER = 2 };
@@ -598,8 +601,8 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     // i -- a scalar load would be waited for by every LDS wait of the tile,
     // since scalar loads return out of order and share the LDS counter)
     constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
-    uint32_t pw[SW], pn[SW] = {}, ppv;
-    auto prefetch = [&](uint32_t tt) {
+    uint32_t pw[SW], pn[SW] = {}, ppv = 0;
+    auto prefetch = [&](uint32_t tt, bool with_pv) {
         tt = (uint32_t)__builtin_amdgcn_readfirstlane((int)tt);
         const uint64_t tw = (uint64_t)tt * TB / 32, pa = tw >= HB / 4 ? tw - HB / 4 : 0u;   // (tile 0: unused)
         const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tw, geo.nwords);
@@ -609,7 +612,7 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
         fs_load<SW>(pw, rs, ln * SW);
         if (HH_CNT_PNX) fs_load<SW>(pn, rs, (ln + 1) * SW);
-        ppv = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (ln % (HB / 4))), 0, 0);
+        if (with_pv) ppv = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (ln % (HB / 4))), 0, 0);
     };
     CDIAG_DECL
     if (t == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
@@ -673,19 +676,29 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
         CDIAG_FLUSH(wk.dbg);
         return;
     }
-    if (t < tend) prefetch(t);
-    uint32_t hin = HIN_NONE;
+    // The bytes before a tile (pv) are needed by the first tile of a run only
+    // (TAIL: every tile): read once before the loop, the loop's loads are the
+    // words alone -- reading pv in the loop had every tile wait for all of
+    // its memory operations (vmcnt(0)), the previous tile's stores included.
+    if (t < tend) prefetch(t, true);
+    uint32_t hin = HIN_NONE, pv[HB / 4];
+    if (!TAIL) {
+#pragma unroll
+        for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
+    }
     for (; t < tend; t += tstep) {
         t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-        uint32_t w[SW], nx[SW], pv[HB / 4];
+        uint32_t w[SW], nx[SW];
 #pragma unroll
         for (uint32_t k = 0; k < SW; k++) {
             w[k] = pw[k];
             nx[k] = pn[k];
         }
+        if (TAIL) {
 #pragma unroll
-        for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
-        prefetch(t + tstep < tend ? t + tstep : t);
+            for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
+        }
+        prefetch(t + tstep < tend ? t + tstep : t, TAIL);
         const uint32_t h63 = cnt_tile<SW, TAIL, CB>(smem, F, g, geo, wk, (uint64_t)t, w, nx, pv, hin CDIAG_PASS);
         hin = TAIL ? HIN_NONE : (uint32_t)__builtin_amdgcn_readfirstlane((int)h63);
     }
@@ -795,9 +808,12 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
 // The emission chain of one region (state, output dword, shift) while it
 // stores each step's symbols into the staging: every step's symbols are
 // shifted into the current dword, which is stored to its aligned LDS address
-// every step (a dword is stored again until it is full: no branch).  The
-// unused bytes of every stored dword are zero: a dword shared with the
+// when it is full (the last, partial one after the last step).  The unused
+// bytes of every stored dword are zero: a dword shared with the
 // neighbouring runs is repaired by OR afterwards (emf_edges).
+#ifndef HH_EMF_STFULL
+#define HH_EMF_STFULL 1       // k_emf: a step stores its dword only when full (0: every step)
+#endif
 #ifndef EMF_KE
 #define EMF_KE 8          // steps within which the first dword is captured
 #endif
@@ -822,8 +838,11 @@ struct EmfChain {
         const uint32_t an = (lo << sh) | a;
         uint32_t sp = __builtin_amdgcn_alignbit(0u, lo, (0u - sh) & 31u);
         if (K != 6) sp = sh ? sp : 0u;
-        *(uint32_t *)(lds + wd) = an;
         const bool full = u >= 32;
+        // the dword once it is full (the run's last, partial one at the end):
+        // an exec-masked store's LDS cycles count its active lanes' addresses
+        // only, and a dword fills every 2.5 steps on kjv
+        if (!HH_EMF_STFULL || full) *(uint32_t *)(lds + wd) = an;
         a = full ? sp : an;
         wd += full ? 4u : 0u;
         sh = u & 31u;
@@ -944,14 +963,15 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
 // (flags[6], k_fscan2): as many waves of the workgroup are active as the
 // LDS beside the tables holds NCH tile stagings for (up to EW), so that
 // typical streams keep more chains in flight than a worst-case size allows.
-// SCO: the tree bounds every tile's output by EMF_COI KiB (the host checks),
-// so the copy-out is EMF_COI unrolled lane-masked 16-B stores and no tile
-// takes the direct path: the number of stores per tile is a compile-time
-// constant, and the next tile's wait for its prefetched words (vmcnt counts
-// loads and stores in order) need not wait for this tile's stores to reach
-// memory -- with a data-dependent store loop it must (30 % of the kernel's
-// wave cycles were that wait).
-#define EMF_COI 16
+// SCO (static copy-out): the copy-out is COI unrolled lane-masked 16-B
+// stores per lane, COI in {4, 8, 16} KiB per tile chosen from this decode's
+// largest tile output (flags[6]) -- the number of stores per tile is a
+// compile-time constant, so the next tile's wait for its prefetched words
+// (vmcnt counts loads and stores in order) need not wait for this tile's
+// stores to reach memory.  With a data-dependent store loop it must: the
+// compiler waits vmcnt(0) at every tile's start (30 % of the kernel's wave
+// cycles in the HH_DIAG build).  (Round 3 measured a fixed COI of 16 no
+// faster: three quarters of its stores were empty.)
 template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO>
 __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1,
@@ -982,129 +1002,146 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
     if (wv >= nact) return;                          // (no workgroup barrier after this point)
     const uint32_t obw = pool / (NCH * nact) & ~15u;
 
-    const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * nact;
-    // next tiles' words, records, corrections and bases, loaded one step
-    // ahead (the base words by lanes 0..2, read out with readlane where consumed)
-    uint32_t pw[NCH][SW], prec[NCH], pfx[NCH], pmeta[NCH];
-    auto prefetch = [&](uint64_t tt0) {
-#pragma unroll
-        for (uint32_t c = 0; c < NCH; c++) {
-            uint64_t tt = tt0 + c * nwv;
-            tt = uni64(tt < t1 ? tt : tt0);
-            const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
-            prec[c] = wk.rec[tt * NR + j];
-            pfx[c] = wk.fx[tt * FX_W + (j & (FX_W - 1))];
-            const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / SCAN_TB);
-            const uint32_t ln = j & 3u;
-            pmeta[c] = *(ln == 0 ? blk32 : ln == 1 ? blk32 + 1 : (const uint32_t *)&wk.lex[tt]);
-            fs_load<SW>(pw[c], rs, j * SW);
+    // the tile loop, with COI unrolled 16-B copy-out stores per lane (a
+    // compile-time count: see above) or (COI = 0) a loop over the tile's bytes
+    auto tiles = [&](auto coi) {
+    constexpr uint32_t COI = decltype(coi)::value;
+        const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * nact;
+        // next tiles' words, records, corrections and bases, loaded one step
+        // ahead (the base words by lanes 0..2, read out with readlane where consumed)
+        uint32_t pw[NCH][SW], prec[NCH], pfx[NCH], pmeta[NCH];
+        auto prefetch = [&](uint64_t tt0) {
+    #pragma unroll
+            for (uint32_t c = 0; c < NCH; c++) {
+                uint64_t tt = tt0 + c * nwv;
+                tt = uni64(tt < t1 ? tt : tt0);
+                const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
+                prec[c] = wk.rec[tt * NR + j];
+                pfx[c] = wk.fx[tt * FX_W + (j & (FX_W - 1))];
+                const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / SCAN_TB);
+                const uint32_t ln = j & 3u;
+                pmeta[c] = *(ln == 0 ? blk32 : ln == 1 ? blk32 + 1 : (const uint32_t *)&wk.lex[tt]);
+                fs_load<SW>(pw[c], rs, j * SW);
+            }
+        };
+        uint64_t t = t0 + (uint64_t)blockIdx.x * nact + wv;
+        EDIAG_DECL
+        if (t < t1) prefetch(t);
+        // (the first tile's loads complete here, once per wave: the compiler
+        // orders them differently before the loop than inside it, and its
+        // wait at the loop head, merged over both paths, was vmcnt(0) --
+        // every tile waiting for the previous tile's stores)
+        __builtin_amdgcn_s_waitcnt(VMCNT0);
+        for (; t < t1; t += NCH * nwv) {
+            uint32_t w[NCH][SW], ent[NCH], c[NCH], L[NCH], Tout[NCH], a0[NCH], oa[NCH], lim = S;
+            uint64_t P0[NCH];
+            bool at_end[NCH], fit[NCH], live[NCH];
+    #pragma unroll
+            for (uint32_t x = 0; x < NCH; x++) {
+    #pragma unroll
+                for (uint32_t k = 0; k < SW; k++) w[x][k] = pw[x][k];
+                const uint64_t tx = t + x * nwv;
+                live[x] = tx < t1;
+                const uint32_t rc = prec[x], fx = j < FX_W ? pfx[x] : 0u;
+                const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)pmeta[x], 0);
+                const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)pmeta[x], 1);
+                const int32_t lx = __builtin_amdgcn_readlane((int)pmeta[x], 2);
+                ent[x] = fsm_rec_ent(rc);
+                int32_t cn = (int32_t)fsm_rec_cnt(rc);
+                if (fsm_fx_ok(fx)) {
+                    ent[x] = fsm_fx_ent(fx);
+                    cn += fsm_fx_d(fx);
+                }
+                c[x] = live[x] ? (uint32_t)cn : 0u;
+                const int32_t incl = wave_incl_scan((int32_t)c[x]);
+                L[x] = (uint32_t)incl - c[x];
+                Tout[x] = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
+                P0[x] = (uint64_t)((int64_t)(((uint64_t)bhi << 32) | blo) + lx);
+                const bool inside = P0[x] <= cap && Tout[x] <= cap - P0[x];
+                // (a tile past the capacity: the host reports it, total > cap)
+                live[x] = live[x] && inside;
+                const uint64_t R = tx * TB + (uint64_t)j * S;
+                at_end[x] = R + S == geo.bits;
+                if (TAIL) {
+                    lim = R >= geo.bits ? 0u : (geo.bits - R < S ? (uint32_t)(geo.bits - R) : S);
+                    at_end[x] = R < geo.bits && R + S >= geo.bits;
+                }
+                a0[x] = (uint32_t)(P0[x] & 15u);
+                fit[x] = a0[x] + Tout[x] + 8 <= obw;
+                // (a chain that does not write its staging still runs: its lanes
+                // all store at the slot's start, inside the slot)
+                oa[x] = tabb + (wv * NCH + x) * obw + (live[x] && fit[x] ? a0[x] + L[x] : 0u);
+            }
+            prefetch(t + NCH * nwv < t1 ? t + NCH * nwv : t);
+            uint32_t fw[NCH], lw[NCH], lwd[NCH];
+            bool fok[NCH];
+            WAVE_SYNC();                                  // the previous tiles' copy-out has read the staging
+            EDIAG_STAMP(0);
+            emf_region<SW, K, TAIL, NCH>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, fw, fok, lw, lwd);
+            WAVE_SYNC();
+            EDIAG_STAMP(1);
+    #pragma unroll
+            for (uint32_t x = 0; x < NCH; x++)
+                if (live[x] && fit[x]) emf_edges<SW, K>(smem, s_b1, s_ts, w[x], ent[x], lim, at_end[x], c[x], oa[x], fw[x], fok[x], lw[x], lwd[x]);
+            WAVE_SYNC();
+            EDIAG_STAMP(2);
+    #pragma unroll
+            for (uint32_t x = 0; x < NCH; x++) {
+                if (!(COI != 0) && !live[x]) continue;      // ((COI != 0): no branch around the stores; a dead tile's resource is empty)
+                if ((COI != 0) || fit[x]) {
+                    // copy-out: whole 16-B blocks; the bytes of the partial first
+                    // and last blocks one per lane (lanes 0..15, 16..31)
+                    uint8_t *gb = out + (P0[x] - a0[x]);
+                    const uint8_t *sb = smem + tabb + (wv * NCH + x) * obw;
+                    const uint32_t end = a0[x] + Tout[x], nq = (end + 15u) / 16u;
+                    const bool part0 = a0[x] != 0 || end < 16, partl = (end & 15u) != 0 && end > 16;
+                    const uint32_t q = j < 16 ? j : (end & ~15u) + (j - 16);
+                    const bool pb = j < 32 && (j < 16 ? part0 : partl) && q >= a0[x] && q < end;
+                    if ((COI != 0)) {
+                        // unconditional buffer stores: the resource spans the
+                        // tile's bytes [0, end), so the hardware drops a store
+                        // past it; lanes with nothing to store get an offset
+                        // past it too -- no branch, a fixed number of stores
+                        const __amdgpu_buffer_rsrc_t ors =
+                            __builtin_amdgcn_make_buffer_rsrc(gb, 0, (int)(live[x] ? end : 0u), 0x00020000);
+    #pragma unroll
+                        for (uint32_t ii = 0; ii < COI; ii++) {
+                            const uint32_t lo = 16 * (j + 64 * ii);
+                            u32x4 v = {0u, 0u, 0u, 0u};
+                            if (lo < end) v = *(const u32x4 *)(sb + lo);   // (LDS reads only where the tile has bytes)
+                            __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(lo >= a0[x] ? lo : 0x40000000u), 0, 0);
+                        }
+                        __builtin_amdgcn_raw_buffer_store_b8(sb[q], ors, (int)(pb ? q : 0x40000000u), 0, 0);
+                    } else {
+                        // four blocks per lane per pass: their LDS reads issued
+                        // together, one wait, then their stores
+                        for (uint32_t i0 = j; i0 < nq; i0 += 256) {
+                            u32x4 v[4];
+    #pragma unroll
+                            for (uint32_t u = 0; u < 4; u++)   // (unconditional: past the tile's bytes they read
+                                v[u] = *(const u32x4 *)(sb + 16 * (i0 + 64 * u));   // what is never stored)
+    #pragma unroll
+                            for (uint32_t u = 0; u < 4; u++) {
+                                const uint32_t lo = 16 * (i0 + 64 * u);
+                                if (lo >= a0[x] && lo + 16 <= end) __builtin_nontemporal_store(v[u], (u32x4 *)(gb + lo));
+                            }
+                        }
+                        if (pb) gb[q] = sb[q];
+                    }
+                } else {
+                    emf_direct<SW>(s_b1, s_ts, w[x], ent[x], lim, at_end[x], out + P0[x] + L[x]);
+                }
+            }
+            EDIAG_STAMP(3);
         }
     };
-    uint64_t t = t0 + (uint64_t)blockIdx.x * nact + wv;
-    EDIAG_DECL
-    if (t < t1) prefetch(t);
-    for (; t < t1; t += NCH * nwv) {
-        uint32_t w[NCH][SW], ent[NCH], c[NCH], L[NCH], Tout[NCH], a0[NCH], oa[NCH], lim = S;
-        uint64_t P0[NCH];
-        bool at_end[NCH], fit[NCH], live[NCH];
-#pragma unroll
-        for (uint32_t x = 0; x < NCH; x++) {
-#pragma unroll
-            for (uint32_t k = 0; k < SW; k++) w[x][k] = pw[x][k];
-            const uint64_t tx = t + x * nwv;
-            live[x] = tx < t1;
-            const uint32_t rc = prec[x], fx = j < FX_W ? pfx[x] : 0u;
-            const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)pmeta[x], 0);
-            const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)pmeta[x], 1);
-            const int32_t lx = __builtin_amdgcn_readlane((int)pmeta[x], 2);
-            ent[x] = fsm_rec_ent(rc);
-            int32_t cn = (int32_t)fsm_rec_cnt(rc);
-            if (fsm_fx_ok(fx)) {
-                ent[x] = fsm_fx_ent(fx);
-                cn += fsm_fx_d(fx);
-            }
-            c[x] = live[x] ? (uint32_t)cn : 0u;
-            const int32_t incl = wave_incl_scan((int32_t)c[x]);
-            L[x] = (uint32_t)incl - c[x];
-            Tout[x] = (uint32_t)__builtin_amdgcn_readlane(incl, 63);
-            P0[x] = (uint64_t)((int64_t)(((uint64_t)bhi << 32) | blo) + lx);
-            const bool inside = P0[x] <= cap && Tout[x] <= cap - P0[x];
-            // (a tile past the capacity: the host reports it, total > cap)
-            live[x] = live[x] && inside;
-            const uint64_t R = tx * TB + (uint64_t)j * S;
-            at_end[x] = R + S == geo.bits;
-            if (TAIL) {
-                lim = R >= geo.bits ? 0u : (geo.bits - R < S ? (uint32_t)(geo.bits - R) : S);
-                at_end[x] = R < geo.bits && R + S >= geo.bits;
-            }
-            a0[x] = (uint32_t)(P0[x] & 15u);
-            fit[x] = a0[x] + Tout[x] + 8 <= obw;
-            // (a chain that does not write its staging still runs: its lanes
-            // all store at the slot's start, inside the slot)
-            oa[x] = tabb + (wv * NCH + x) * obw + (live[x] && fit[x] ? a0[x] + L[x] : 0u);
-        }
-        prefetch(t + NCH * nwv < t1 ? t + NCH * nwv : t);
-        uint32_t fw[NCH], lw[NCH], lwd[NCH];
-        bool fok[NCH];
-        WAVE_SYNC();                                  // the previous tiles' copy-out has read the staging
-        EDIAG_STAMP(0);
-        emf_region<SW, K, TAIL, NCH>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, fw, fok, lw, lwd);
-        WAVE_SYNC();
-        EDIAG_STAMP(1);
-#pragma unroll
-        for (uint32_t x = 0; x < NCH; x++)
-            if (live[x] && fit[x]) emf_edges<SW, K>(smem, s_b1, s_ts, w[x], ent[x], lim, at_end[x], c[x], oa[x], fw[x], fok[x], lw[x], lwd[x]);
-        WAVE_SYNC();
-        EDIAG_STAMP(2);
-#pragma unroll
-        for (uint32_t x = 0; x < NCH; x++) {
-            if (!SCO && !live[x]) continue;      // (SCO: no branch around the stores; a dead tile's resource is empty)
-            if (SCO || fit[x]) {
-                // copy-out: whole 16-B blocks; the bytes of the partial first
-                // and last blocks one per lane (lanes 0..15, 16..31)
-                uint8_t *gb = out + (P0[x] - a0[x]);
-                const uint8_t *sb = smem + tabb + (wv * NCH + x) * obw;
-                const uint32_t end = a0[x] + Tout[x], nq = (end + 15u) / 16u;
-                const bool part0 = a0[x] != 0 || end < 16, partl = (end & 15u) != 0 && end > 16;
-                const uint32_t q = j < 16 ? j : (end & ~15u) + (j - 16);
-                const bool pb = j < 32 && (j < 16 ? part0 : partl) && q >= a0[x] && q < end;
-                if (SCO) {
-                    // unconditional buffer stores: the resource spans the
-                    // tile's bytes [0, end), so the hardware drops a store
-                    // past it; lanes with nothing to store get an offset
-                    // past it too -- no branch, a fixed number of stores
-                    const __amdgpu_buffer_rsrc_t ors =
-                        __builtin_amdgcn_make_buffer_rsrc(gb, 0, (int)(live[x] ? end : 0u), 0x00020000);
-#pragma unroll
-                    for (uint32_t ii = 0; ii < EMF_COI; ii++) {
-                        const uint32_t lo = 16 * (j + 64 * ii);
-                        u32x4 v = {0u, 0u, 0u, 0u};
-                        if (lo < end) v = *(const u32x4 *)(sb + lo);   // (LDS reads only where the tile has bytes)
-                        __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(lo >= a0[x] ? lo : 0x40000000u), 0, 0);
-                    }
-                    __builtin_amdgcn_raw_buffer_store_b8(sb[q], ors, (int)(pb ? q : 0x40000000u), 0, 0);
-                } else {
-                    // four blocks per lane per pass: their LDS reads issued
-                    // together, one wait, then their stores
-                    for (uint32_t i0 = j; i0 < nq; i0 += 256) {
-                        u32x4 v[4];
-#pragma unroll
-                        for (uint32_t u = 0; u < 4; u++)   // (unconditional: past the tile's bytes they read
-                            v[u] = *(const u32x4 *)(sb + 16 * (i0 + 64 * u));   // what is never stored)
-#pragma unroll
-                        for (uint32_t u = 0; u < 4; u++) {
-                            const uint32_t lo = 16 * (i0 + 64 * u);
-                            if (lo >= a0[x] && lo + 16 <= end) __builtin_nontemporal_store(v[u], (u32x4 *)(gb + lo));
-                        }
-                    }
-                    if (pb) gb[q] = sb[q];
-                }
-            } else {
-                emf_direct<SW>(s_b1, s_ts, w[x], ent[x], lim, at_end[x], out + P0[x] + L[x]);
-            }
-        }
-        EDIAG_STAMP(3);
-    }
+    // COI from this decode's largest tile output: the copy-out of a tile of
+    // mx symbols at a 16-B misalignment < 16 is at most (mx + 15) / 16 blocks
+    const uint32_t per = (mx + 15u + 16u * 64u - 1u) / (16u * 64u);
+    if (!TAIL && SCO && per <= 4) tiles(std::integral_constant<uint32_t, 4>{});
+    else if (!TAIL && SCO && per <= 8) tiles(std::integral_constant<uint32_t, 8>{});
+    else if (!TAIL && SCO && per <= 16) tiles(std::integral_constant<uint32_t, 16>{});
+    else tiles(std::integral_constant<uint32_t, 0>{});
     EDIAG_FLUSH(wk.dbg);
 }
 
@@ -1186,10 +1223,9 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen) 
     fd->r = F->r;
     fd->S = F->S;
     fd->G = G;
-    // every tile's output is at most 64 S / minlen symbols (+ the tail rule's)
-    // (measured no faster than the store loop -- the time moved from the
-    // wait at the tile start into the stores -- so it is opt-in: HH_EMF_SCO)
-    fd->sco = tmax + 16u + 8u + 15u <= (uint64_t)EMF_COI * 1024u && getenv("HH_EMF_SCO");
+    // the static copy-out (k_emf, SCO) unless HH_EMF_SCO=0; k_emf falls back
+    // to the store loop itself for tiles of more than 16 KiB
+    fd->sco = !(getenv("HH_EMF_SCO") && atoi(getenv("HH_EMF_SCO")) == 0);
     FS_OK(hipMalloc(&fd->ct, (size_t)ns << (F->cb + 1)));
     FS_OK(hipMalloc(&fd->b1, (size_t)ns * 8));
     FS_OK(hipMalloc(&fd->tsym, (size_t)ns + 1));
