@@ -1607,7 +1607,7 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
         uint32_t Gf = hh_fsm_pick_head(d->ht, d->S, d->ft->cb);
         if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) / d->ft->cb * d->ft->cb;   // experiments
         if (Gf > d->S) Gf = 0;
-        const int urc = fsm_upload(&d->fsm, d->ft, Gf, (uint32_t)d->ht->minlen);
+        const int urc = fsm_upload(&d->fsm, d->ft, Gf, (uint32_t)d->ht->minlen, (uint32_t)d->ht->maxlen);
         d->fsm.dbg = d->d_dbg;
         if (urc != HH_OK && urc != HH_ERR_UNSUPPORTED) return urc;
     }

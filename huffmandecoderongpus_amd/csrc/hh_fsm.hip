@@ -817,7 +817,36 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
 #ifndef EMF_KE
 #define EMF_KE 8          // steps within which the first dword is captured
 #endif
-template <uint32_t K>
+// Staging swizzle (SWZ, near-uniform codes): the dword at LDS byte address a
+// is kept at a ^ (((a >> 7) & 31) << 2), i.e. dwords are permuted within
+// each aligned 128-B chunk by the chunk's index.  Where every region emits
+// the same number of bytes (2-bit codes: 128 B per 256-bit region) the 64
+// lanes' runs start 32 dwords apart and every step's stores would fall in
+// one bank; swizzled, lane j's dword p is in bank p ^ j.  The copy-out reads
+// a chunk's 16-B blocks back in order (emf_unswz).
+template <bool SWZ>
+__device__ __forceinline__ uint32_t emf_swz(uint32_t a) { return SWZ ? a ^ ((a >> 5) & 0x7cu) : a; }
+
+// The 16 bytes at LDS offset a (a multiple of 16) in order: with SWZ the
+// 128-B chunk's key moves the block (key bits 2..4) and permutes its dwords
+// (bits 0..1).
+template <bool SWZ>
+__device__ __forceinline__ u32x4 emf_read16(const uint8_t *lds, uint32_t a) {
+    if (!SWZ) return *(const u32x4 *)(lds + a);
+    const uint32_t key = (a >> 7) & 31u;
+    const u32x4 v = *(const u32x4 *)(lds + (a ^ ((key & 28u) << 2)));
+    const bool s1 = key & 1u, s2 = key & 2u;
+    // logical dword t is at position t ^ (key & 3)
+    const uint32_t x0 = s1 ? v.y : v.x, x1 = s1 ? v.x : v.y, x2 = s1 ? v.w : v.z, x3 = s1 ? v.z : v.w;
+    u32x4 o;
+    o.x = s2 ? x2 : x0;
+    o.y = s2 ? x3 : x1;
+    o.z = s2 ? x0 : x2;
+    o.w = s2 ? x1 : x3;
+    return o;
+}
+
+template <uint32_t K, bool SWZ = false>
 struct EmfChain {
     uint32_t row, wd0, wd, sh, a, fw, wdk;
     __device__ __forceinline__ void init(uint32_t s, uint32_t oa) {
@@ -842,7 +871,7 @@ struct EmfChain {
         // the dword once it is full (the run's last, partial one at the end):
         // an exec-masked store's LDS cycles count its active lanes' addresses
         // only, and a dword fills every 2.5 steps on kjv
-        if (!HH_EMF_STFULL || full) *(uint32_t *)(lds + wd) = an;
+        if (!HH_EMF_STFULL || full) *(uint32_t *)(lds + emf_swz<SWZ>(wd)) = an;
         a = full ? sp : an;
         wd += full ? 4u : 0u;
         sh = u & 31u;
@@ -865,13 +894,13 @@ struct EmfChain {
 // the r-bit step (r = S mod K); TAIL (NCH = 1): steps while whole, the rest
 // bit by bit, and the tail rule.  *first: the run's bytes in its first dword
 // (valid when *first_ok), *lastw / *lastwd: the run's last dword.
-template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH>
+template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SWZ = false>
 __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const uint32_t *b1, const uint8_t *ts,
                                            const uint32_t (*w)[SW], const uint32_t *s, uint32_t lim,
                                            const bool *at_end, const uint32_t *oa, uint32_t *first, bool *first_ok,
                                            uint32_t *lastw, uint32_t *lastwd) {
     constexpr uint32_t S = 32 * SW, r = S % K;
-    EmfChain<K> ch[NCH];
+    EmfChain<K, SWZ> ch[NCH];
 #pragma unroll
     for (uint32_t c = 0; c < NCH; c++) ch[c].init(s[c], oa[c]);
 #pragma unroll
@@ -890,7 +919,7 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
     }
 #pragma unroll
     for (uint32_t c = 0; c < NCH; c++) {
-        EmfChain<K> &x = ch[c];
+        EmfChain<K, SWZ> &x = ch[c];
         if (!TAIL) {
             if (r) {
                 const uint64_t e = *(const uint64_t *)(lds + er_off + (x.row >> (K - r)) + (rbits<SW>(w[c], S - r, r) << 3));
@@ -907,7 +936,7 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
             x.row = st << (K + 3);
         }
         if (at_end[c] && (x.row >> (K + 3)) != 0) x.put(lds, HH_FSM_ET_MAKE(ts[x.row >> (K + 3)], 0u, 1u));   // the tail rule
-        *(uint32_t *)(lds + x.wd) = x.a;               // the bytes of the last step's overflow
+        *(uint32_t *)(lds + emf_swz<SWZ>(x.wd)) = x.a;   // the bytes of the last step's overflow
         // the first dword: complete in fw once the run left it within EMF_KE
         // steps; the final dword when the run never left it
         first[c] = x.wd == x.wd0 ? x.a : x.fw;
@@ -921,7 +950,7 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
 // one run's bytes (and zeros); each run ORs its own bytes back into its first
 // and last dword.  The first dword's bytes were captured by emf_region (a
 // bit-serial re-run when the run left its first dword late).
-template <uint32_t SW, uint32_t K>
+template <uint32_t SW, uint32_t K, bool SWZ = false>
 __device__ __forceinline__ void emf_edges(uint8_t *lds, const uint32_t *b1, const uint8_t *ts, const uint32_t *w,
                                           uint32_t s, uint32_t lim, bool at_end, uint32_t cnt, uint32_t oa,
                                           uint32_t first, bool first_ok, uint32_t lastw, uint32_t lastwd) {
@@ -939,8 +968,8 @@ __device__ __forceinline__ void emf_edges(uint8_t *lds, const uint32_t *b1, cons
         if (got < need && at_end && st != 0) acc |= (uint32_t)ts[st] << (8 * got++);
         firstw = acc << (8 * b0);
     }
-    atomicOr((uint32_t *)(lds + (oa & ~3u)), firstw);
-    if (lastwd != (oa & ~3u) && lastw) atomicOr((uint32_t *)(lds + lastwd), lastw);
+    atomicOr((uint32_t *)(lds + emf_swz<SWZ>(oa & ~3u)), firstw);
+    if (lastwd != (oa & ~3u) && lastw) atomicOr((uint32_t *)(lds + emf_swz<SWZ>(lastwd)), lastw);
 }
 
 // A region whose tile's output does not fit the staging buffer: its symbols
@@ -972,11 +1001,12 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
 // compiler waits vmcnt(0) at every tile's start (30 % of the kernel's wave
 // cycles in the HH_DIAG build).  (Round 3 measured a fixed COI of 16 no
 // faster: three quarters of its stores were empty.)
-template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO>
+template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO, bool SWZ = false>
 __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1,
                                                  uint32_t lds_bytes) {
     static_assert(!TAIL || NCH == 1, "the tail tiles take one chain per lane");
+    static_assert(!SWZ || !TAIL, "the tail tiles' staging is not swizzled");
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW;
     const uint32_t ns = geo.ns, r = geo.r, tid = threadIdx.x, j = tid & 63u;
@@ -992,15 +1022,16 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
     __syncthreads();
     // staging per tile: the largest tile output + its 16-B misalignment + the
     // last step's overflow dword; the active waves share the rest of the LDS
-    const uint32_t tabb = emf_tab_bytes(ns, K, r);
+    const uint32_t tabb = SWZ ? (emf_tab_bytes(ns, K, r) + 127u) & ~127u : emf_tab_bytes(ns, K, r);   // (SWZ: 128-B chunks)
     const uint32_t pool = lds_bytes > tabb ? lds_bytes - tabb : 0u;
     const uint32_t mx = __builtin_amdgcn_readfirstlane((int)wk.flags[6]);
-    const uint32_t need = (mx + 16u + 8u + 15u) & ~15u;
+    constexpr uint32_t SU = SWZ ? 128u : 16u;         // staging slot unit (SWZ: whole 128-B chunks)
+    const uint32_t need = (mx + 16u + 8u + SU - 1u) & ~(SU - 1u);
     uint32_t nact = pool / (NCH * need);
     nact = nact > EW ? EW : nact < 1u ? 1u : nact;
     if (nact > blockDim.x / 64u) nact = blockDim.x / 64u;
     if (wv >= nact) return;                          // (no workgroup barrier after this point)
-    const uint32_t obw = pool / (NCH * nact) & ~15u;
+    const uint32_t obw = pool / (NCH * nact) & ~(SU - 1u);   // (>= need: need is a multiple of SU)
 
     // the tile loop, with COI unrolled 16-B copy-out stores per lane (a
     // compile-time count: see above) or (COI = 0) a loop over the tile's bytes
@@ -1077,12 +1108,12 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
             bool fok[NCH];
             WAVE_SYNC();                                  // the previous tiles' copy-out has read the staging
             EDIAG_STAMP(0);
-            emf_region<SW, K, TAIL, NCH>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, fw, fok, lw, lwd);
+            emf_region<SW, K, TAIL, NCH, SWZ>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, fw, fok, lw, lwd);
             WAVE_SYNC();
             EDIAG_STAMP(1);
     #pragma unroll
             for (uint32_t x = 0; x < NCH; x++)
-                if (live[x] && fit[x]) emf_edges<SW, K>(smem, s_b1, s_ts, w[x], ent[x], lim, at_end[x], c[x], oa[x], fw[x], fok[x], lw[x], lwd[x]);
+                if (live[x] && fit[x]) emf_edges<SW, K, SWZ>(smem, s_b1, s_ts, w[x], ent[x], lim, at_end[x], c[x], oa[x], fw[x], fok[x], lw[x], lwd[x]);
             WAVE_SYNC();
             EDIAG_STAMP(2);
     #pragma unroll
@@ -1108,10 +1139,10 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
                         for (uint32_t ii = 0; ii < COI; ii++) {
                             const uint32_t lo = 16 * (j + 64 * ii);
                             u32x4 v = {0u, 0u, 0u, 0u};
-                            if (lo < end) v = *(const u32x4 *)(sb + lo);   // (LDS reads only where the tile has bytes)
+                            if (lo < end) v = emf_read16<SWZ>(smem, (uint32_t)(sb - smem) + lo);   // (LDS reads only where the tile has bytes)
                             __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(lo >= a0[x] ? lo : 0x40000000u), 0, 0);
                         }
-                        __builtin_amdgcn_raw_buffer_store_b8(sb[q], ors, (int)(pb ? q : 0x40000000u), 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b8(smem[emf_swz<SWZ>((uint32_t)(sb - smem) + q)], ors, (int)(pb ? q : 0x40000000u), 0, 0);
                     } else {
                         // four blocks per lane per pass: their LDS reads issued
                         // together, one wait, then their stores
@@ -1119,14 +1150,14 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
                             u32x4 v[4];
     #pragma unroll
                             for (uint32_t u = 0; u < 4; u++)   // (unconditional: past the tile's bytes they read
-                                v[u] = *(const u32x4 *)(sb + 16 * (i0 + 64 * u));   // what is never stored)
+                                v[u] = emf_read16<SWZ>(smem, (uint32_t)(sb - smem) + 16 * (i0 + 64 * u));   // what is never stored)
     #pragma unroll
                             for (uint32_t u = 0; u < 4; u++) {
                                 const uint32_t lo = 16 * (i0 + 64 * u);
                                 if (lo >= a0[x] && lo + 16 <= end) __builtin_nontemporal_store(v[u], (u32x4 *)(gb + lo));
                             }
                         }
-                        if (pb) gb[q] = sb[q];
+                        if (pb) gb[q] = smem[emf_swz<SWZ>((uint32_t)(sb - smem) + q)];
                     }
                 } else {
                     emf_direct<SW>(s_b1, s_ts, w[x], ent[x], lim, at_end[x], out + P0[x] + L[x]);
@@ -1165,11 +1196,13 @@ static kcnt_t kcnt_for(uint32_t sw, bool tail, uint32_t cb) {
 }
 // chains per lane of the main emission launch
 static uint32_t emf_nch() { return 1u; }
-static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sco) {
+// (swz: the swizzled staging, with the static copy-out)
+static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sco, bool swz = false) {
     (void)nch;   // (two chains per lane: measured slower, not instantiated)
     switch (sw) {
-#define EMF_K(n, k)                                                                      \
-    (tail ? k_emf<n, k, true, 1, false> : sco ? k_emf<n, k, false, 1, true> : k_emf<n, k, false, 1, false>)
+#define EMF_K(n, k)                                                                                       \
+    (tail ? k_emf<n, k, true, 1, false> : swz ? k_emf<n, k, false, 1, true, true>                         \
+                                        : sco ? k_emf<n, k, false, 1, true> : k_emf<n, k, false, 1, false>)
 #define X(n)                                                                            \
     case n:                                                                             \
         return K == 7 ? EMF_K(n, 7) : K == 6 ? EMF_K(n, 6) : K == 4 ? EMF_K(n, 4) : nullptr;
@@ -1203,7 +1236,7 @@ void fsm_free(FsmDev *fd) {
     memset(fd, 0, sizeof(*fd));
 }
 
-int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen) {
+int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, uint32_t maxlen) {
     fsm_free(fd);
     const uint32_t ns = F->ns;
     const uint32_t sw = F->S / 32;
@@ -1226,6 +1259,17 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen) 
     // the static copy-out (k_emf, SCO) unless HH_EMF_SCO=0; k_emf falls back
     // to the store loop itself for tiles of more than 16 KiB
     fd->sco = !(getenv("HH_EMF_SCO") && atoi(getenv("HH_EMF_SCO")) == 0);
+    // regions of a code whose lengths differ by at most one bit emit nearly
+    // the same number of bytes each: lanes' runs start a fixed stride apart
+    // and their stores collide in one bank unless the staging is swizzled
+    // (HH_EMF_SWZ=0/1 overrides)
+    fd->swz = maxlen <= minlen + 1;
+    if (getenv("HH_EMF_SWZ")) fd->swz = atoi(getenv("HH_EMF_SWZ")) != 0;
+    // (the swizzled staging rounds the tables and a tile's staging up to
+    // 128 B: one staging of the largest tile output must still fit)
+    if (fd->swz && ((uint64_t)((emf_tab_bytes(ns, F->K, F->r) + 127u) & ~127u) + ((tmax + 16u + 8u + 127u) & ~127ull) >
+                    EMF_LDS || !fd->sco))
+        fd->swz = 0;
     FS_OK(hipMalloc(&fd->ct, (size_t)ns << (F->cb + 1)));
     FS_OK(hipMalloc(&fd->b1, (size_t)ns * 8));
     FS_OK(hipMalloc(&fd->tsym, (size_t)ns + 1));
@@ -1242,11 +1286,11 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen) 
 
 static int fsm_grids(FsmDev *fd) {
     if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns && fd->sized_K == fd->K && fd->sized_sco == fd->sco &&
-        fd->sized_cb == fd->cb)
+        fd->sized_cb == fd->cb && fd->sized_swz == fd->swz)
         return HH_OK;
     const uint32_t sw = fd->S / 32;
     const kcnt_t kc = kcnt_for(sw, false, fd->cb);
-    const kemf_t ke = kemf_for(sw, fd->K, false, emf_nch(), fd->sco);
+    const kemf_t ke = kemf_for(sw, fd->K, false, emf_nch(), fd->sco, fd->swz);
     if (!kc || !ke) return HH_ERR_UNSUPPORTED;
     int pc = 0, pe = 0, ncu = 0, dev = 0;
     FS_OK(hipGetDevice(&dev));
@@ -1260,6 +1304,7 @@ static int fsm_grids(FsmDev *fd) {
     fd->sized_ns = fd->ns;
     fd->sized_K = fd->K;
     fd->sized_sco = fd->sco;
+    fd->sized_swz = fd->swz;
     fd->sized_cb = fd->cb;
     return HH_OK;
 }
@@ -1372,7 +1417,7 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
         if (ne > emit_from) {
             const uint64_t nwg = (ne - emit_from + ew - 1) / ew;
             const uint32_t ge = (uint32_t)(nwg < fd->grid_e ? nwg : fd->grid_e);
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch(), fd->sco), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch(), fd->sco, fd->swz), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne,
                                (uint32_t)lds_emf(fd));
             FS_OK(hipGetLastError());

@@ -19,8 +19,9 @@ struct FsmDev {
     uint8_t *tsym;
     uint64_t *et, *er;
     // persistent grids (workgroups), sized by the occupancy API for S / ns
-    uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K, sized_sco, sized_cb;
-    uint32_t sco;            // k_emf's static copy-out (every tile output <= 16 KiB by the tree)
+    uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K, sized_sco, sized_cb, sized_swz;
+    uint32_t sco;            // k_emf's static copy-out (the default; HH_EMF_SCO=0: the store loop)
+    uint32_t swz;            // k_emf's swizzled staging: codes whose lengths differ by at most 1 bit
     uint64_t *dbg;           // HH_DIAG builds: phase cycles of k_cnt (16 x u64, the decoder's)
 };
 
@@ -44,7 +45,7 @@ void fsm_ws_free(FsmWs *ws);
 int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
                hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms);
-int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen);
+int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, uint32_t maxlen);
 bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile);   // 7-bit steps leave room for 16 stagings
 void fsm_free(FsmDev *fd);
 int fsm_debug_arrays(const FsmWs *ws, uint64_t nt, uint32_t *rec, uint32_t *fx, int32_t *tsum, uint32_t *xs);

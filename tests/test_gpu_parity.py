@@ -315,6 +315,53 @@ def test_walk_bound_and_deferral_lists(hh, files_dir, env, monkeypatch):
         dec.close()
 
 
+@pytest.mark.parametrize("env", [{"HH_EMF_SWZ": "1"}, {"HH_EMF_SWZ": "0"}, {"HH_EMF_SCO": "0"},
+                                 {"HH_EMF_SCO": "0", "HH_EMF_SWZ": "1"}])
+def test_emission_staging_variants(hh, files_dir, env, monkeypatch):
+    """k_emf's staging and copy-out variants give the same bytes: the
+    swizzled staging (chosen for near-uniform codes) forced on kjv's
+    variable-length code and off on E.coli's 2-bit code, and the copy-out
+    loop instead of the static copy-out (its counted stores) -- each on the
+    kjv-tiled and E.coli-tiled streams through the state machine and on
+    cut streams of a random tree against the oracle."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)                # read when the tree is set
+    for src in ("kjv.txt", "E.coli"):
+        hf, text = synth.load_source(files_dir, src)
+        syn = synth.tiled_stream(hf, text, 16 << 20)
+        dec = hh.Decoder(0, flags=hh.FLAG_NO_FIXED)
+        try:
+            dec.set_tree(syn.tree)
+            out = torch.full((syn.decoded_bytes + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+            n = dec.decode_device(syn.data, syn.bits, out)
+            torch.cuda.synchronize()
+            st = dec.stats()
+            assert st["state_machine"] == 1 and st["exact_fallback"] == 0, (src, st)
+            assert n == syn.decoded_bytes, src
+            assert synth.verify_tiled(out, syn), src
+            assert int(out[n:n + 64].ne(0xAB).sum()) == 0, src
+        finally:
+            dec.close()
+    rng = np.random.default_rng(77)
+    iz, io, sy, syms = _random_tree(rng, 40)
+    p = rng.dirichlet(np.full(40, 0.5))
+    t = hh.Tree(iz, io, sy)
+    text = rng.choice(syms, size=300_000, p=p).astype(np.uint8)
+    data, bits = t.encode(text)
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(t)
+        for cut in (bits, bits - 1, bits // 3 + 7):
+            ref = _oracle(iz, io, sy, data, cut)
+            got = _decode_dev(hh, dec, data, cut, cut + 16)
+            assert dec.stats()["state_machine"] == 1
+            assert len(got) == len(ref) and np.array_equal(got, ref), cut
+    finally:
+        dec.close()
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_fixture_legacy_pipeline(hh, files_dir, name):
     """Every fixture through round 2's pipeline (HH_FLAG_LEGACY), device
