@@ -108,8 +108,9 @@ def cpu_baseline(files_dir: str, seconds: float, name: str = "kjv.txt.huff") -> 
 def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, steps: int,
                     warmup: int) -> dict:
     """One more single-GPU workload, device-resident like the headline one:
-    correctness first, then `steps` timed decodes (kernel time from the
-    decoder's HIP events, wall time around the loop)."""
+    correctness first, then `steps` timed decodes as a stream of
+    asynchronous decodes (kernel time from the decoder's HIP events, wall
+    time around the loop, every decode's length checked)."""
     import torch
     n = dec.decode_device(data, bits, out)
     torch.cuda.synchronize()
@@ -117,13 +118,17 @@ def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, s
     for _ in range(warmup):
         dec.decode_device(data, bits, out)
     torch.cuda.synchronize()
-    st = []
+    st, lens = [], []
     t0 = time.perf_counter()
     for _ in range(steps):
-        dec.decode_device(data, bits, out)
-        st.append(dec.stats())
+        lens.append(dec.decode_device_async(data, bits, out))   # (as the headline loop)
+        if len(lens) > 1:
+            st.append(dec.stats())
+    dec.wait()
+    st.append(dec.stats())
     torch.cuda.synchronize()
     ms_step = (time.perf_counter() - t0) / steps * 1e3
+    ok = ok and all(int(x.value) == n_want for x in lens)
     ms_dev = statistics.mean(s["ms_total"] for s in st)
     C = (bits + 7) // 8
     ach = (C + n_want) / (ms_dev * 1e-3) / 1e9
@@ -267,6 +272,11 @@ def main():
         def run_step():
             return dec.decode_device(syn.data, syn.bits, out, stream)
 
+        def run_step_async():
+            # enqueues this decode and checks the previous one (its length,
+            # status and device times) while this one runs
+            return dec.decode_device_async(syn.data, syn.bits, out, stream)
+
     # correctness of the measured configuration, outside the timed region
     n = run_step()
     torch.cuda.synchronize()
@@ -281,19 +291,41 @@ def main():
     for _ in range(a.warmup):
         run_step()
     torch.cuda.synchronize()
+    sync_ms = None
+    if world == 1:
+        # the synchronous call (hh_decode_device: returns once the length is
+        # known) timed on its own, for the per-call latency
+        ts = []
+        for _ in range(max(3, a.steps // 2)):
+            t1 = time.perf_counter()
+            run_step()
+            ts.append(time.perf_counter() - t1)
+        sync_ms = statistics.median(ts) * 1e3
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    dev_ms = []
+    dev_ms, lens = [], []
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        run_step()
+    if world == 1:
+        # a stream of decodes: each enqueued while the previous one runs and
+        # is checked (hh_decode_device_async), the last checked by the wait
+        for _ in range(a.steps):
+            lens.append(run_step_async())
+            if len(lens) > 1:
+                dev_ms.append(dec.stats())      # (the decode checked by this call)
+        dec.wait()
         dev_ms.append(dec.stats())
+    else:
+        for _ in range(a.steps):
+            run_step()
+            dev_ms.append(dec.stats())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if world == 1 and any(int(n.value) != syn.decoded_bytes for n in lens):
+        raise SystemExit("a timed decode returned the wrong length")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -341,6 +373,7 @@ def main():
                      "ms_front": phases["sync"], "ms_scan": phases["scan"],
                      "ms_emit": phases["emit"]},
         "decoded_MBps_device": round(D_bytes / (ms_dev * 1e-3) / 1e6, 1),
+        "ms_per_call_sync": round(sync_ms, 4) if sync_ms is not None else None,
         "fast_path": fast,
         "state_machine_path": all(s["state_machine"] == 1 for s in dev_ms),
     }

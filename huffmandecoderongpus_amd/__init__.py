@@ -101,6 +101,9 @@ _SIGS = {
     "hh_decoder_stats": ([C.c_void_p, C.POINTER(_Stats)], C.c_int),
     "hh_decode_device": ([C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                           C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
+    "hh_decode_device_async": ([C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
+    "hh_decode_wait": ([C.c_void_p], C.c_int),
     "hh_decoder_tile_bits": ([C.c_void_p, C.POINTER(C.c_uint64)], C.c_int),
     "hh_decode_device_range": ([C.c_void_p, C.c_void_p, C.POINTER(_Range), C.c_void_p,
                                 C.c_uint64, C.POINTER(_RangeOut), C.c_void_p], C.c_int),
@@ -241,11 +244,13 @@ class Decoder:
         _check(lib().hh_decoder_create(C.byref(self._h), C.byref(cfg)), "decoder create")
         self.device = device
         self._tree = None
+        self._pending = []          # buffers of asynchronous decodes, kept alive until wait()
 
     def close(self):
         if self._h:
-            lib().hh_decoder_destroy(self._h)
+            lib().hh_decoder_destroy(self._h)   # (waits for an asynchronous decode still running)
             self._h = C.c_void_p()
+        self._pending = []
 
     def __del__(self):
         try:
@@ -291,6 +296,28 @@ class Decoder:
         s = stream if stream is not None else torch.cuda.current_stream(data.device)
         return self.decode_device_ptr(data.data_ptr(), bits, out.data_ptr(), out.numel(),
                                       s.cuda_stream)
+
+    def decode_device_async(self, data, bits: int, out, stream=None) -> "C.c_uint64":
+        """hh_decode_device_async on torch tensors: enqueues the decode and
+        returns a c_uint64 that holds its length once checked (by the next
+        asynchronous decode or by wait()).  data, out and the returned
+        object must live until wait() returns."""
+        import torch
+        assert data.is_cuda and out.is_cuda and data.dtype == torch.uint8
+        assert data.numel() >= (bits + 7) // 8 + PAYLOAD_PAD
+        s = stream if stream is not None else torch.cuda.current_stream(data.device)
+        n = C.c_uint64(0)
+        self._pending.append((data, out, n))
+        _check(lib().hh_decode_device_async(self._h, data.data_ptr(), bits, out.data_ptr(), out.numel(),
+                                            C.byref(n), s.cuda_stream), "decode_device_async")
+        return n
+
+    def wait(self) -> None:
+        """hh_decode_wait: every asynchronous decode checked; raises the first
+        failure among them."""
+        rc = lib().hh_decode_wait(self._h)
+        self._pending = []
+        _check(rc, "decode_wait")
 
     def tile_bits(self) -> int:
         """Bits per tile for the current tree (segments are whole tiles)."""

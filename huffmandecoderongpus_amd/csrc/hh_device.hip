@@ -1389,6 +1389,7 @@ struct hh_decoder {
     int32_t *d_max;      // findmax result (stage API)
     uint64_t *d_dbg;     // HH_DIAG counters (16 x u64)
     hipEvent_t ev[4];
+    hipEvent_t ev2[4];         // result slot 1's events (an asynchronous decode behind another)
     hh_stats stats;
     uint32_t grid_f, grid_e, grid_w, grid_x;   // persistent grid sizes (occupancy x CUs)
     uint32_t fwalk;            // k_front's walk bound (HH_FRONT_WALK overrides)
@@ -1416,7 +1417,22 @@ struct hh_decoder {
     hipStream_t h2d, d2h;
     hipEvent_t *pipe_ev;
     uint32_t npipe_ev;
+    // the asynchronous decode not checked yet (hh_decode_device_async)
+    struct {
+        int active;
+        int fixed;             // a k_fixed launch (the length was known at launch)
+        FsmPend pd;
+        const void *d_data;
+        uint64_t bits;
+        void *d_out;
+        uint64_t *out_len;
+        hipStream_t st;
+    } apend;
+    int async_rc;              // the first failure since the last hh_decode_wait
+    uint32_t async_seq;        // asynchronous decodes launched (the result slot alternates)
 };
+
+static int async_check(hh_decoder *d);
 
 static int ensure_dev(void **p, size_t *have, size_t need) {
     if (*have >= need) return HH_OK;
@@ -1460,7 +1476,7 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
         return HH_ERR_DEVICE;
     }
     for (int i = 0; i < 4; i++) {
-        if (hipEventCreate(&d->ev[i]) != hipSuccess) {
+        if (hipEventCreate(&d->ev[i]) != hipSuccess || hipEventCreate(&d->ev2[i]) != hipSuccess) {
             hh_decoder_destroy(d);
             return HH_ERR_DEVICE;
         }
@@ -1472,6 +1488,7 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
 extern "C" void hh_decoder_destroy(hh_decoder *d) {
     if (!d) return;
     hipSetDevice(d->device);
+    async_check(d);                     // (an asynchronous decode still running)
     if (d->ws) hipFree(d->ws);
     if (d->d_l1) hipFree(d->d_l1);
     if (d->d_l2) hipFree(d->d_l2);
@@ -1490,8 +1507,10 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
         hipEventDestroy(d->h_ev[1]);
     }
     if (d->h_flags) hipHostFree(d->h_flags);
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < 4; i++) {
         if (d->ev[i]) hipEventDestroy(d->ev[i]);
+        if (d->ev2[i]) hipEventDestroy(d->ev2[i]);
+    }
     if (d->stream) hipStreamDestroy(d->stream);
     fsm_free(&d->fsm);
     fsm_ws_free(&d->fsm_ws);
@@ -1527,6 +1546,8 @@ static uint32_t pick_region_bits(const hh_tables *t, int req) {
 
 extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     if (!d || !tree) return HH_ERR_ARG;
+    HIP_OK(hipSetDevice(d->device));
+    async_check(d);                     // (a pending asynchronous decode uses the current tables)
     int rc = hh_tables_build(tree, d->ht);
     if (rc) return rc;
     HIP_OK(hipSetDevice(d->device));
@@ -1970,8 +1991,10 @@ out:
 }
 
 // A complete fixed-length code: k_fixed (above).
+// (ev: the events of the launch; wait = false: returns once enqueued)
 static int fixed_path(hh_decoder *d, const void *d_data, uint64_t bits, uint8_t *d_out, uint64_t cap,
-                      uint64_t *out_len, hipStream_t st) {
+                      uint64_t *out_len, hipStream_t st, hipEvent_t *ev = nullptr, bool wait = true) {
+    if (!ev) ev = d->ev;
     const uint32_t L = d->fixed_len;
     const uint64_t nsym = bits / L + (bits % L ? 1 : 0);
     *out_len = nsym;
@@ -1981,14 +2004,15 @@ static int fixed_path(hh_decoder *d, const void *d_data, uint64_t bits, uint8_t 
     const uint64_t nthr = (nsym + 15) / 16, cap_blk = (uint64_t)(d->ncu ? d->ncu : 256) * 32;
     uint64_t nb = (nthr + 255) / 256;
     if (nb > cap_blk) nb = cap_blk;
-    HIP_OK(hipEventRecord(d->ev[0], st));
+    HIP_OK(hipEventRecord(ev[0], st));
     hipLaunchKernelGGL(k_fixed, dim3((unsigned)nb), dim3(256), 0, st, (const uint32_t *)d_data, bits, L,
                        (const uint8_t *)d->d_fsym, d->tab, d_out, nsym);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipEventRecord(d->ev[3], st));
-    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipEventRecord(ev[3], st));
+    if (!wait) return HH_OK;
+    HIP_OK(hipEventSynchronize(ev[3]));
     float ms = 0;
-    hipEventElapsedTime(&ms, d->ev[0], d->ev[3]);
+    hipEventElapsedTime(&ms, ev[0], ev[3]);
     d->stats.ms_emit = ms;
     d->stats.ms_total = ms;
     return HH_OK;
@@ -2018,6 +2042,7 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     // work, e.g. torch's), never the decoder's private non-blocking stream
     hipStream_t st = (hipStream_t)hip_stream;
     HIP_OK(hipSetDevice(d->device));
+    async_check(d);                     // (an asynchronous decode before it: its status is kept for hh_decode_wait)
     memset(&d->stats, 0, sizeof(d->stats));
     *out_len = 0;
     if (bits == 0) return HH_OK;
@@ -2068,6 +2093,106 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     return rc;
 }
 
+// ---------------------------------------------------------------------------
+// Asynchronous decodes (hh_decode_device_async / hh_decode_wait): a decode is
+// enqueued and the PREVIOUS one checked, so that the GPU has the next decode
+// queued while the host reads the last one's results (from its own result
+// slot and event set: the two alternate).
+// ---------------------------------------------------------------------------
+static hipEvent_t *slot_ev(hh_decoder *d, uint32_t slot) { return slot ? d->ev2 : d->ev; }
+
+// Check the pending asynchronous decode: its length to *out_len, its status
+// kept in async_rc (the first failure).  A stream that did not resynchronise
+// is decoded again here, on the exact path, as hh_decode_device would.
+static int async_check(hh_decoder *d) {
+    if (!d->apend.active) return HH_OK;
+    d->apend.active = 0;
+    hipEvent_t *ev = slot_ev(d, d->apend.pd.slot);
+    int rc;
+    memset(&d->stats, 0, sizeof(d->stats));
+    if (d->apend.fixed) {
+        rc = hipEventSynchronize(ev[3]) == hipSuccess ? HH_OK : HH_ERR_DEVICE;
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev[0], ev[3]);
+        d->stats.ms_emit = d->stats.ms_total = ms;
+        d->stats.fixed_length = 1;
+        d->stats.out_len = *d->apend.out_len;
+    } else {
+        uint64_t total = 0;
+        uint32_t leave = 0, en = 0;
+        float ms[3] = {0, 0, 0};
+        rc = fsm_collect(&d->fsm_ws, ev, &d->apend.pd, &total, &leave, &en, ms);
+        fsm_stats(d, d->apend.bits, total, ms);
+        *d->apend.out_len = total;
+        if (rc == HH_NOSYNC) {
+            d->stats.repairs = 1;
+            const bool seg_ok = d->ht->maxlen <= HH_MAXLEN_FAST && !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
+            d->stats.exact_fallback = seg_ok ? 2 : 1;
+            rc = seg_ok ? segment_path(d, d->apend.d_data, d->apend.bits, (uint8_t *)d->apend.d_out, d->apend.pd.cap,
+                                       d->apend.out_len, d->apend.st)
+                        : stage_pipeline(d, d->apend.d_data, (int64_t)d->apend.bits, (uint8_t *)d->apend.d_out,
+                                         d->apend.pd.cap, d->apend.out_len, d->apend.st);
+        }
+    }
+    if (rc != HH_OK && d->async_rc == HH_OK) d->async_rc = rc;
+    return rc;
+}
+
+extern "C" int hh_decode_device_async(hh_decoder *d, const void *d_data, uint64_t bits, void *d_out,
+                                      uint64_t cap, uint64_t *out_len, void *hip_stream) {
+    if (!d || !out_len || (!d_data && bits) || (!d_out && cap)) return HH_ERR_ARG;
+    if (!d->have_tree) return HH_ERR_ARG;
+    if (((uintptr_t)d_data & 3u) != 0) return HH_ERR_ARG;
+    hipStream_t st = (hipStream_t)hip_stream;
+    HIP_OK(hipSetDevice(d->device));
+    *out_len = 0;
+    const bool fixed = d->fixed_len && !(d->cfg.flags & (HH_FLAG_NO_FIXED | HH_FLAG_FORCE_EXACT | HH_FLAG_FORCE_SEGMENT));
+    if (bits == 0 || !(fixed || fsm_path_ok(d))) {
+        // the other paths decode synchronously (the pending decode first)
+        async_check(d);
+        const int rc = hh_decode_device(d, d_data, bits, d_out, cap, out_len, hip_stream);
+        if (rc != HH_OK && d->async_rc == HH_OK) d->async_rc = rc;
+        return HH_OK;
+    }
+    // the previous decode's slot and events stay untouched until it is checked
+    const uint32_t slot = d->apend.active ? (d->apend.pd.slot ^ 1u) : 0u;
+    FsmPend pd;
+    memset(&pd, 0, sizeof(pd));
+    pd.slot = slot;
+    int rc;
+    if (fixed) {
+        uint64_t n = 0;
+        rc = fixed_path(d, d_data, bits, (uint8_t *)d_out, cap, &n, st, slot_ev(d, slot), false);
+        *out_len = n;
+    } else {
+        rc = fsm_launch(&d->fsm, &d->fsm_ws, slot, slot_ev(d, slot), d_data, bits, 0, 0, 0, d_out, cap, st, &pd);
+    }
+    async_check(d);                     // the previous decode, while this one runs
+    if (rc != HH_OK) {
+        if (d->async_rc == HH_OK) d->async_rc = rc;
+        return rc == HH_ERR_CAPACITY ? HH_OK : rc;   // (a capacity failure is reported by hh_decode_wait)
+    }
+    d->apend.active = 1;
+    d->apend.fixed = fixed;
+    d->apend.pd = pd;
+    d->apend.d_data = d_data;
+    d->apend.bits = bits;
+    d->apend.d_out = d_out;
+    d->apend.out_len = out_len;
+    d->apend.st = st;
+    d->async_seq++;
+    return HH_OK;
+}
+
+extern "C" int hh_decode_wait(hh_decoder *d) {
+    if (!d) return HH_ERR_ARG;
+    HIP_OK(hipSetDevice(d->device));
+    async_check(d);
+    const int rc = d->async_rc;
+    d->async_rc = HH_OK;
+    return rc;
+}
+
 extern "C" int hh_decoder_tile_bits(const hh_decoder *d, uint64_t *tile_bits) {
     if (!d || !tile_bits || !d->have_tree) return HH_ERR_ARG;
     *tile_bits = (uint64_t)HH_NR * d->S;
@@ -2082,6 +2207,7 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
     if (((uintptr_t)d_data & 3u) != 0) return HH_ERR_ARG;
     hipStream_t st = (hipStream_t)hip_stream;
     HIP_OK(hipSetDevice(d->device));
+    async_check(d);
     memset(&d->stats, 0, sizeof(d->stats));
     memset(ro, 0, sizeof(*ro));
     ro->leave_state = ro->entry_state = rg->in_state;
@@ -2264,6 +2390,7 @@ extern "C" int hh_decode_host(hh_decoder *d, const uint8_t *data, uint64_t bits,
                               uint64_t cap, uint64_t *out_len) {
     if (!d || !out_len || (!data && bits) || (!out && cap)) return HH_ERR_ARG;
     HIP_OK(hipSetDevice(d->device));
+    async_check(d);
     *out_len = 0;
     const uint64_t nb = (bits + 7) / 8;
     const uint64_t ocap = cap ? cap : 1;

@@ -1311,7 +1311,10 @@ static int fsm_grids(FsmDev *fd) {
 
 static int ws_need(FsmWs *ws, size_t need) {
     if (ws->size >= need) return HH_OK;
-    if (ws->p) FS_OK(hipFree(ws->p));
+    if (ws->p) {
+        FS_OK(hipDeviceSynchronize());   // (an asynchronous decode may still use it)
+        FS_OK(hipFree(ws->p));
+    }
     ws->p = nullptr;
     ws->size = 0;
     const size_t sz = need + need / 8;
@@ -1329,7 +1332,7 @@ void fsm_ws_free(FsmWs *ws) {
 
 static int ws_side(FsmWs *ws) {
     if (ws->h_res) return HH_OK;
-    if (hipHostMalloc((void **)&ws->h_res, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    if (hipHostMalloc((void **)&ws->h_res, FSM_RES_SLOTS * 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         ws->h_res = nullptr;
         return HH_ERR_NOMEM;
     }
@@ -1337,10 +1340,14 @@ static int ws_side(FsmWs *ws) {
     return HH_OK;
 }
 
-int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
-               uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
-               hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms) {
+// The launch half: every kernel of the decode enqueued on st, the results
+// to be written by k_fscan2 into result slot `slot` of the host-mapped
+// memory; *pd keeps what fsm_collect needs.
+int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void *d_data, uint64_t bits,
+               uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap, hipStream_t st,
+               FsmPend *pd) {
     if (!fd->ok) return HH_ERR_UNSUPPORTED;
+    if (slot >= FSM_RES_SLOTS) return HH_ERR_ARG;
     int rc = fsm_grids(fd);
     if (rc) return rc;
     if (in_state >= fd->ns) return HH_ERR_ARG;
@@ -1382,7 +1389,6 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
 #endif
     rc = ws_side(ws);
     if (rc) return rc;
-    (void)h_flags;
     FS_OK(hipEventRecord(ev[0], st));
     {
         // tiles [0, nc) whose regions and next region end before the stream,
@@ -1407,7 +1413,7 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     FS_OK(hipEventRecord(ev[1], st));
     hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk);
     FS_OK(hipGetLastError());
-    hipLaunchKernelGGL(k_fscan2, dim3(1), dim3(1024), 0, st, geo, wk, nblk, ws->d_res);
+    hipLaunchKernelGGL(k_fscan2, dim3(1), dim3(1024), 0, st, geo, wk, nblk, ws->d_res + 16 * slot);
     FS_OK(hipGetLastError());
     FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
@@ -1430,8 +1436,20 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
         }
     }
     FS_OK(hipEventRecord(ev[3], st));
-    FS_OK(hipStreamSynchronize(st));
-    const volatile uint32_t *res = ws->h_res;
+    pd->nt = nt;
+    pd->emit_from = emit_from;
+    pd->cap = cap;
+    pd->slot = slot;
+    return HH_OK;
+}
+
+// The collect half: waits for the decode's last kernel (its end event) and
+// reads its results from its slot.
+int fsm_collect(FsmWs *ws, hipEvent_t *ev, const FsmPend *pd, uint64_t *total, uint32_t *leave, uint32_t *entry,
+                float *ms) {
+    FS_OK(hipEventSynchronize(ev[3]));
+    const uint64_t nt = pd->nt, emit_from = pd->emit_from, cap = pd->cap;
+    const volatile uint32_t *res = ws->h_res + 16 * pd->slot;
     const uint32_t fl = res[0];
     *total = (uint64_t)res[2] | ((uint64_t)res[3] << 32);
     *leave = res[4];
@@ -1443,6 +1461,16 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
     if (fl & FF_FAIL) return HH_NOSYNC;
     if (*total > cap) return HH_ERR_CAPACITY;
     return HH_OK;
+}
+
+int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
+               uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
+               hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms) {
+    (void)h_flags;
+    FsmPend pd;
+    const int rc = fsm_launch(fd, ws, 0, ev, d_data, bits, ntiles, in_state, emit_from, d_out, cap, st, &pd);
+    if (rc) return rc;
+    return fsm_collect(ws, ev, &pd, total, leave, entry, ms);
 }
 
 // Diagnostic: the count pass's arrays of the last decode (tests, tools).

@@ -38,13 +38,29 @@ struct FsmWs {
     void *p;
     size_t size;
     // the decode's results (status, total, leave / entry state), written by
-    // k_fscan2 straight into host-mapped memory: no copy, no memset per decode
+    // k_fscan2 straight into host-mapped memory: no copy, no memset per
+    // decode.  FSM_RES_SLOTS slots of 16 words: a decode in flight and the
+    // next one enqueued behind it (hh_decode_device_async) keep theirs apart.
     uint32_t *h_res, *d_res;
+};
+#define FSM_RES_SLOTS 2
+// What fsm_collect needs of a decode fsm_launch enqueued.
+struct FsmPend {
+    uint64_t nt, emit_from, cap;
+    uint32_t slot;
 };
 void fsm_ws_free(FsmWs *ws);
 int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
                hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms);
+// fsm_decode in two halves: fsm_launch enqueues the decode (results into
+// slot `slot`, events ev[0..3]) and returns; fsm_collect waits for its end
+// event and returns what fsm_decode would.
+int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void *d_data, uint64_t bits,
+               uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap, hipStream_t st,
+               FsmPend *pd);
+int fsm_collect(FsmWs *ws, hipEvent_t *ev, const FsmPend *pd, uint64_t *total, uint32_t *leave, uint32_t *entry,
+                float *ms);
 int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, uint32_t maxlen);
 bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile);   // 7-bit steps leave room for 16 stagings
 void fsm_free(FsmDev *fd);

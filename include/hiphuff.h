@@ -182,6 +182,25 @@ int hh_decode_device(hh_decoder *dec, const void *d_data, uint64_t bits,
                      void *d_out, uint64_t cap, uint64_t *out_len,
                      void *hip_stream);
 
+/* Asynchronous form of hh_decode_device for a stream of decodes: enqueues
+ * the decode on `hip_stream` and returns before it has run, then checks the
+ * decode issued before it (its length into the out_len pointer passed with
+ * it), so that the GPU has the next decode queued while the host reads the
+ * last one's results instead of idling between synchronous calls.
+ * hh_decode_wait checks the last one and returns the first failure of the
+ * asynchronous decodes since the previous wait (HH_OK if none), as
+ * hh_decode_device would have returned it; a stream that does not
+ * resynchronise is decoded again on the exact path there.  Every out_len
+ * pointer and output buffer must stay valid until hh_decode_wait returns.
+ * The call itself returns HH_OK, or the argument / launch failure of this
+ * decode.  Paths other than the state machine and k_fixed decode
+ * synchronously inside the call.  Other entry points (hh_decode_device,
+ * ranges, host decodes) first check a pending asynchronous decode. */
+int hh_decode_device_async(hh_decoder *dec, const void *d_data, uint64_t bits,
+                           void *d_out, uint64_t cap, uint64_t *out_len,
+                           void *hip_stream);
+int hh_decode_wait(hh_decoder *dec);
+
 /* ---------------------------------------------------------------------- */
 /* Segments (multi-GPU shards).  The stream is cut into tiles of           */
 /* hh_decoder_tile_bits() bits; a segment is a run of whole tiles.  The    */

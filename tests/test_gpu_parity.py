@@ -769,6 +769,75 @@ def test_segment_path_fixtures(hh, files_dir, name):
         dec.close()
 
 
+def test_async_decodes(hh, files_dir):
+    """hh_decode_device_async / hh_decode_wait: decodes of different streams
+    enqueued back to back, each checked while the next runs (alternating
+    result slots) -- the state machine (kjv), k_fixed (E.coli), a random tree's
+    cut stream, and the same decoder reused -- every output and length
+    byte-exact against the oracle after the wait; a capacity failure among
+    them is reported by the wait (the others still decode), and synchronous
+    calls after asynchronous ones see a drained decoder."""
+    import torch
+    jobs = []
+    for name in ("kjv.txt", "E.coli", "paper1"):
+        path = os.path.join(files_dir, name + ".huff")
+        hf = hh.HuffFile.load(path)
+        jobs.append((hf.tree(), hf.data, hf.bits, O.OracleHuff.load(path).chain_decode()))
+    rng = np.random.default_rng(31)
+    iz, io, sy, syms = _random_tree(rng, 60)
+    t = hh.Tree(iz, io, sy)
+    data, bits = t.encode(rng.choice(syms, size=400_000, p=rng.dirichlet(np.full(60, 0.4))).astype(np.uint8))
+    for cut in (bits, bits // 2 + 3):
+        jobs.append((t, data, cut, _oracle(iz, io, sy, data, cut)))
+    decs = {}
+    try:
+        for rep in range(2):
+            pend = []
+            for k, (tree, data, bits, ref) in enumerate(jobs):
+                dec = decs.get(k % 3)
+                if dec is None:
+                    dec = decs[k % 3] = hh.Decoder(0)
+                dec.set_tree(tree)
+                buf = np.zeros(((bits + 7) // 8 + 64 + 3) // 4 * 4, np.uint8)
+                buf[: (bits + 7) // 8] = np.asarray(data, np.uint8)[: (bits + 7) // 8]
+                d_in = torch.from_numpy(buf).cuda()
+                d_out = torch.full((len(ref) + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+                # the same decoder twice in a row: two decodes in flight on it
+                for _ in range(2):
+                    n = dec.decode_device_async(d_in, bits, d_out)
+                    pend.append((dec, n, d_out, ref))
+                dec.wait() if rep == 1 else None
+            for dec in decs.values():
+                dec.wait()
+            for dec, n, d_out, ref in pend:
+                assert n.value == len(ref)
+                got = d_out[: n.value].cpu().numpy()
+                assert np.array_equal(got, ref)
+                assert int(d_out[n.value: n.value + 64].ne(0xAB).sum()) == 0
+        # a capacity failure is the wait's; the decode after it is fine
+        tree, data, bits, ref = jobs[0]
+        dec = decs[0]
+        dec.set_tree(tree)
+        buf = np.zeros(((bits + 7) // 8 + 64 + 3) // 4 * 4, np.uint8)
+        buf[: (bits + 7) // 8] = np.asarray(data, np.uint8)[: (bits + 7) // 8]
+        d_in = torch.from_numpy(buf).cuda()
+        small = torch.zeros(len(ref) // 2, dtype=torch.uint8, device="cuda")
+        d_out = torch.zeros(len(ref) + 64, dtype=torch.uint8, device="cuda")
+        dec.decode_device_async(d_in, bits, small)
+        n = dec.decode_device_async(d_in, bits, d_out)
+        with pytest.raises(hh.HipHuffError):
+            dec.wait()
+        assert n.value == len(ref) and np.array_equal(d_out[: n.value].cpu().numpy(), ref)
+        dec.wait()                                      # (cleared)
+        # a synchronous decode right after an asynchronous one
+        dec.decode_device_async(d_in, bits, d_out)
+        assert dec.decode_device(d_in, bits, d_out) == len(ref)
+        dec.wait()
+    finally:
+        for dec in decs.values():
+            dec.close()
+
+
 def test_non_resynchronising_code_takes_the_segment_path(hh):
     """An 11-bit fixed-length code with 96-bit regions realigns only every 11
     regions (> HH_KM): the walks fail and the decoder must switch to the
