@@ -98,11 +98,76 @@ def cpu_baseline(files_dir: str, seconds: float, name: str = "kjv.txt.huff") -> 
                     break
     except OSError:
         pass
-    return {"value": round(D / med / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": kind,
+    return {"value": round(D / med / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": kind, "jumpbits": best_j,
             "sample": (f"linApproach(jumpbits={best_j}) on files/{name} "
                        f"({D} B decoded), median of {len(times)} runs over ~{seconds:.0f} s, "
                        f"tables built inside each timed call; host {cpu}, "
                        f"nproc {os.cpu_count()}")}
+
+
+_CPU_CHILD = """
+import sys, time
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as O
+h = O.RefHuff(sys.argv[2])
+t0 = float(sys.argv[5])
+while time.time() < t0:        # (every process loaded: all start together)
+    time.sleep(0.001)
+for _ in range(int(sys.argv[4])):
+    h.run("linApproach", int(sys.argv[3]))
+print(time.time(), flush=True)
+"""
+
+
+def cpu_baseline_tiled(H, hf, text, mib: int, jumpbits: int, reps: int, procs: int) -> dict:
+    """The reference's linApproach (oracle/_ref) on the headline stream's
+    shape at the largest size its HUFF header holds (int32 bits: 128 MiB of
+    the kjv-tiled stream, saved as a .huff), jumpbits from the kjv.txt sweep:
+    (a) one core, `reps` repeats, median; (b) `procs` processes on the host's
+    cores at once, each decoding the whole stream twice -- the aggregate rate
+    of independent decodes, the most a host running the reference's serial
+    decoder on many streams gets."""
+    import subprocess
+    import tempfile
+    import numpy as np
+    from oracle import oracle as O
+    from huffmandecoderongpus_amd import synth
+    syn = synth.tiled_stream(hf, text, mib << 20, device="cpu")
+    nb = (syn.bits + 7) // 8
+    data = np.zeros(nb + H.PAYLOAD_PAD, np.uint8)
+    data[:nb] = syn.data[:nb].numpy()
+    D = syn.decoded_bytes
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, f"kjv_tiled_{mib}MiB.huff")
+        H.HuffFile(hf.izero, hf.ione, hf.sym, syn.bits, D, data).save(path)
+        del data, syn
+        h = O.RefHuff(path)
+        out = h.run("linApproach", jumpbits)
+        ok = out.size == D and np.array_equal(out[: text.size], text)
+        del out
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            h.run("linApproach", jumpbits)
+            ts.append(time.perf_counter() - t0)
+        del h
+        t_go = time.time() + 5.0 + 0.2 * procs
+        ps = [subprocess.Popen([sys.executable, "-c", _CPU_CHILD, ROOT, path, str(jumpbits), "2", repr(t_go)],
+                               stdout=subprocess.PIPE, text=True) for _ in range(procs)]
+        outs = [p.communicate()[0] for p in ps]
+        rcs = [p.returncode for p in ps]
+        ends = [float(o.split()[-1]) for o in outs if o.split()]
+        wall = (max(ends) - t_go) if len(ends) == procs else float("nan")
+    med = statistics.median(ts)
+    return {"value": round(D / med / 1e6, 2), "unit": "MB/s", "cores": 1, "ok": bool(ok),
+            "sample": (f"linApproach(jumpbits={jumpbits}) on the {mib} MiB kjv-tiled stream ({D} B decoded; "
+                       f"the largest the HUFF header's int32 bit count holds), median of {reps}"),
+            "processes": {"n": procs, "ok": all(r == 0 for r in rcs),
+                          "value": round(procs * 2 * D / wall / 1e6, 1), "unit": "MB/s",
+                          "wall_s": round(wall, 2),
+                          "sample": (f"{procs} processes started together (after each loaded the "
+                                     f"file), each decoding the whole stream twice; wall time to the "
+                                     f"last one's end; host cores: {os.cpu_count()} visible")}}
 
 
 def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, steps: int,
@@ -445,6 +510,10 @@ def main():
         res["evaluate"] = ev
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.files, a.cpu_seconds)
+        from oracle import oracle as O
+        if O.ref_available():
+            res["cpu_baseline"]["tiled"] = cpu_baseline_tiled(
+                H, hf, text, 128, res["cpu_baseline"]["jumpbits"], 3, min(16, os.cpu_count() or 1))
         if "workloads" in res:
             # beside the E.coli workload: the reference's best jumpbits differs there
             res["workloads"][0]["cpu_baseline"] = cpu_baseline(a.files, a.cpu_seconds, "E.coli.huff")

@@ -38,6 +38,15 @@ for mib in sizes:
         dec.decode_device(syn.data, syn.bits, out)
         ms.append(dec.stats())
     torch.cuda.synchronize()
+    # wall time per decode in a stream of asynchronous decodes (as bench.py)
+    lens = []
+    t1 = time.perf_counter()
+    for _ in range(runs * 4):
+        lens.append(dec.decode_device_async(syn.data, syn.bits, out))
+    dec.wait()
+    torch.cuda.synchronize()
+    ms_step = (time.perf_counter() - t1) / (runs * 4) * 1e3
+    ok = ok and all(int(x.value) == syn.decoded_bytes for x in lens)
     t = statistics.median(s["ms_total"] for s in ms)
     C, D = syn.compressed_bytes, syn.decoded_bytes
     row = {"MiB": mib, "bits": syn.bits, "decoded_bytes": D, "ok": bool(ok),
@@ -46,6 +55,7 @@ for mib in sizes:
            "ms_scan": round(statistics.median(s["ms_scan"] for s in ms), 4),
            "ms_emit": round(statistics.median(s["ms_emit"] for s in ms), 4),
            "decoded_MBps": round(D / (t * 1e-3) / 1e6, 1),
+           "ms_step_async": round(ms_step, 4), "decoded_MBps_wall": round(D / (ms_step * 1e-3) / 1e6, 1),
            "roofline_frac": round((C + D) / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
            "fast_path": all(s["exact_fallback"] == 0 for s in ms)}
     rows.append(row)
