@@ -21,7 +21,7 @@ LIB      := $(PKG)/libhiphuff.so
 CLI      := $(BUILD)/HuffFramework
 EMU      := tests/emu/libhh_emu.so
 
-all: lib cli oracle emu
+all: lib cli oracle emu ubench
 
 lib: $(LIB)
 cli: $(CLI)
@@ -54,6 +54,12 @@ $(CLI): $(PKG)/host/hh_cli.c $(LIB) include/hiphuff.h include/hiphuff_plugin.h
 oracle:
 	$(MAKE) -C oracle
 
+# microbenchmarks the profiling scripts run (tools/profile.sh: FETCH_SIZE
+# calibration on known byte counts)
+ubench: $(BUILD)/ub_fetch
+$(BUILD)/ub_fetch: tools/ubench/ub_fetch.hip | $(BUILD)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -o $@ $<
+
 $(EMU): tests/emu/hh_emu.cpp tests/emu/hh_fsm_emu.cpp $(CSRC)/hh_algo.h $(CSRC)/hh_fsm_algo.h $(CSRC)/hh_fsm.h $(CSRC)/hh_internal.h $(BUILD)/hh_huff.o
 	$(CXX) -O2 -fPIC -shared $(INC) -Wno-comment -o $@ tests/emu/hh_emu.cpp tests/emu/hh_fsm_emu.cpp $(BUILD)/hh_huff.o
 
@@ -61,7 +67,7 @@ clean:
 	rm -rf $(BUILD) $(LIB) $(EMU)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib cli emu oracle clean
+.PHONY: all lib cli emu oracle ubench clean
 
 # A/B variant of the library: make variant V=name HIPEXTRA="-DHH_X=1"
 # -> build/libhiphuff_<name>.so (tools/ab.sh)
