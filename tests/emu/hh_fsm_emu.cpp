@@ -25,6 +25,7 @@
 static hh_tables g_T;
 static hh_fsm_tables g_F;
 static uint32_t g_K = 0;                            // emission step bits asked for (hh_fsm_emu_set_k)
+static uint32_t g_M = 1;                            // regions per lane of the count pass (hh_fsm_emu_set_m)
 static std::vector<uint32_t> g_rec, g_xs, g_fx;   // the last decode's count-pass arrays
 static std::vector<int64_t> g_tsum;
 
@@ -32,6 +33,10 @@ extern "C" {
 
 // The emission step the next decodes build their tables for (0, 6, 7).
 void hh_fsm_emu_set_k(uint32_t K) { g_K = K; }
+// Regions per lane of the count pass (the kernels' k_cnt with M > 1: a lane
+// counts M consecutive regions, its chain carried from one to the next; a
+// head guesses only a lane's first region): tiles of 64 M regions.
+void hh_fsm_emu_set_m(uint32_t M) { g_M = M ? M : 1u; }
 
 // stats[0] tiles  [1] walks  [2] walks not met in their region  [3] S
 // [4] G  [5] next-tile corrections  [6] corrections over > 1 region
@@ -63,38 +68,43 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
     memcpy(wv.data(), data, (bits + 7) / 8);
     // (bits past the end are never read as stream bits)
     const uint32_t *w = wv.data();
-    const uint64_t TB = (uint64_t)NR * S;
+    // (a tile here: 64 lanes x M regions; region j of a tile is lane j / M's)
+    const uint32_t M = g_M, NRT = NR * M;
+    const uint64_t TB = (uint64_t)NRT * S;
     const uint64_t all = (bits + TB - 1) / TB;
     const uint64_t nt = ntiles_req && ntiles_req < all ? ntiles_req : all;
-    std::vector<uint32_t> rec(nt * NR), xs(nt), fx((nt + 1) * HH_FSM_KM, 0u);
+    std::vector<uint32_t> rec(nt * NRT), xs(nt), fx((nt + 1) * HH_FSM_KM, 0u);
     std::vector<int64_t> tsum(nt);
+    std::vector<uint32_t> g(NRT), sp(NRT), n(NRT), tx(NRT), mm(NRT), dp(NRT), u(NRT), ent(NRT), cnt(NRT), xv(NRT);
+    std::vector<int32_t> dl(NRT);
     for (uint64_t t = 0; t < nt; t++) {
         const uint64_t T0 = t * TB;
-        uint32_t g[NR], sp[NR], n[NR], tx[NR], mm[NR], dp[NR], u[NR], ent[NR], cnt[NR], xv[NR];
-        int32_t dl[NR];
-        for (int j = 0; j < NR; j++) {
+        // g[j]: the entry region j+1 is assumed in -- a head guess where
+        // region j+1 starts a lane, else the exit region j's chain reaches
+        for (uint32_t j = 0; j < NRT; j++) {
             const uint64_t R1 = T0 + (uint64_t)(j + 1) * S;
             uint32_t c = 0;
             g[j] = 0;
-            if (G && R1 - G < bits) g[j] = fsm_run(&F, w, R1 - G, R1 < bits ? R1 : bits, 0u, &c);
+            if ((j + 1) % M == 0 && G && R1 - G < bits) g[j] = fsm_run(&F, w, R1 - G, R1 < bits ? R1 : bits, 0u, &c);
         }
         // region 0 of a later tile: the head guess from the G bits before it
-        // (the same chain the previous tile's last lane computed as g[NR-1])
+        // (the same chain the previous tile's last lane computed as g[NRT-1])
         uint32_t h0 = 0;
         if (t > 0 && G) {
             uint32_t c = 0;
             h0 = fsm_run(&F, w, T0 - G, T0, 0u, &c);
         }
-        for (int j = 0; j < NR; j++) {
+        for (uint32_t j = 0; j < NRT; j++) {
+            if (j % M != 0) g[j - 1] = tx[j - 1];     // (a lane's chain carried into its next region)
             sp[j] = j ? g[j - 1] : (t == 0 ? in_state : h0);
             const uint64_t R = T0 + (uint64_t)j * S;
             tx[j] = fsm_region(&F, w, R, R + S, bits, sp[j], &n[j]);
         }
-        for (int j = 0; j < NR; j++) {
+        for (uint32_t j = 0; j < NRT; j++) {
             mm[j] = dp[j] = 0;
             dl[j] = 0;
             u[j] = tx[j];
-            if (j == NR - 1) continue;                 // (the next tile: fsm_fix_next)
+            if (j == NRT - 1) continue;                // (the next tile: fsm_fix_next)
             const uint64_t R = T0 + (uint64_t)(j + 1) * S;
             if (tx[j] == g[j] || R >= bits) continue;
             mm[j] = 1;
@@ -105,18 +115,18 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
             u[j] = A;
             stats[2] += dp[j];
         }
-        for (int j = 0; j < NR; j++) {
+        for (uint32_t j = 0; j < NRT; j++) {
             ent[j] = j ? tx[j - 1] : sp[0];
             cnt[j] = n[j] + (j && mm[j - 1] ? (uint32_t)dl[j - 1] : 0u);
             xv[j] = j && mm[j - 1] && dp[j - 1] ? u[j - 1] : tx[j];
         }
-        uint32_t x = xv[NR - 1];
+        uint32_t x = xv[NRT - 1];
         bool deep = false;
-        for (int j = 0; j < NR; j++) deep = deep || dp[j];
+        for (uint32_t j = 0; j < NRT; j++) deep = deep || dp[j];
         if (deep) {
             // the in-tile fixer (the kernel's rare serial path)
             uint32_t st = xv[0];
-            for (int r = 1; r < NR; r++) {
+            for (uint32_t r = 1; r < NRT; r++) {
                 if (st == ent[r]) {
                     st = xv[r];
                     continue;
@@ -132,14 +142,14 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
         }
         xs[t] = x;
         int64_t sum = 0;
-        for (int j = 0; j < NR; j++) {
-            rec[t * NR + j] = fsm_rec(ent[j], cnt[j]);
+        for (uint32_t j = 0; j < NRT; j++) {
+            rec[t * NRT + j] = fsm_rec(ent[j], cnt[j]);
             sum += cnt[j];
         }
         tsum[t] = sum;
-        if (t + 1 < nt && x != g[NR - 1]) {
+        if (t + 1 < nt && x != g[NRT - 1]) {
             stats[5]++;
-            if (!fsm_fix_next(&F, w, T0 + TB, S, bits, x, g[NR - 1], &fx[(t + 1) * HH_FSM_KM])) return HH_ERR_UNSUPPORTED;
+            if (!fsm_fix_next(&F, w, T0 + TB, S, bits, x, g[NRT - 1], &fx[(t + 1) * HH_FSM_KM])) return HH_ERR_UNSUPPORTED;
             stats[6] += fsm_fx_ok(fx[(t + 1) * HH_FSM_KM + 1]) != 0;
         }
         stats[0]++;
@@ -150,9 +160,9 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
     uint8_t buf[8192];
     for (uint64_t t = prologue; t < nt; t++) {
         const uint64_t T0 = t * TB;
-        for (int j = 0; j < NR; j++) {
-            uint32_t e = fsm_rec_ent(rec[t * NR + j]);
-            int64_t c = fsm_rec_cnt(rec[t * NR + j]);
+        for (uint32_t j = 0; j < NRT; j++) {
+            uint32_t e = fsm_rec_ent(rec[t * NRT + j]);
+            int64_t c = fsm_rec_cnt(rec[t * NRT + j]);
             if (j < HH_FSM_KM && fsm_fx_ok(fx[t * HH_FSM_KM + j])) {
                 e = fsm_fx_ent(fx[t * HH_FSM_KM + j]);
                 c += fsm_fx_d(fx[t * HH_FSM_KM + j]);

@@ -191,11 +191,14 @@ def femu():
     L.hh_fsm_emu_tables.argtypes = [C.c_void_p] * 3 + [C.c_int32, C.c_uint32, C.c_void_p]
     L.hh_fsm_emu_set_k.restype = None
     L.hh_fsm_emu_set_k.argtypes = [C.c_uint32]
+    L.hh_fsm_emu_set_m.restype = None
+    L.hh_fsm_emu_set_m.argtypes = [C.c_uint32]
     return L
 
 
-def run_femu(L, izero, ione, sym, data, bits, S=0, G=-1, ntiles=0, prologue=0, in_state=0, K=0):
+def run_femu(L, izero, ione, sym, data, bits, S=0, G=-1, ntiles=0, prologue=0, in_state=0, K=0, M=1):
     L.hh_fsm_emu_set_k(K)                     # emission step bits (0: the default, 6)
+    L.hh_fsm_emu_set_m(M)                     # regions per lane of the count pass
     iz = np.ascontiguousarray(izero, np.int32)
     io = np.ascontiguousarray(ione, np.int32)
     sy = np.ascontiguousarray(sym, np.uint8)
@@ -231,6 +234,47 @@ def test_fsm_walks_that_meet_late_are_exact(femu):
     n, out, st, _, _ = run_femu(femu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits, 64, 8)
     assert n == len(ref) and np.array_equal(out, ref)
     assert st[2] > 0 and st[6] > 0           # walks past their region; multi-region corrections
+
+
+@pytest.mark.parametrize("M", [2, 4, 8])
+def test_fsm_lanes_of_several_regions(femu, M):
+    """The count pass with M consecutive regions per lane (a head guesses
+    only a lane's first region; the chain is carried through the others):
+    every fixture, and kjv.txt with small regions and short heads so that
+    walks cross several regions of a lane and the next tile's corrections
+    span lanes."""
+    try:
+        _lanes_of_several_regions(femu, M)
+    finally:
+        femu.hh_fsm_emu_set_m(1)              # (the library's setting outlives the test)
+
+
+def _lanes_of_several_regions(femu, M):
+    for name in ("hello", "paper1", "kjv.txt", "E.coli", "world192.txt"):
+        hf = H.HuffFile.load(os.path.join(FILES, name + ".huff"))
+        ref = O.OracleHuff.load(os.path.join(FILES, name + ".huff")).chain_decode()
+        n, out, st, _, _ = run_femu(femu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits, M=M)
+        assert n == len(ref) and np.array_equal(out, ref), (name, n, st)
+    hf = H.HuffFile.load(os.path.join(FILES, "kjv.txt.huff"))
+    ref = O.OracleHuff.load(os.path.join(FILES, "kjv.txt.huff")).chain_decode()
+    n, out, st, _, _ = run_femu(femu, hf.izero, hf.ione, hf.sym, hf.payload, hf.bits, 64, 8, M=M)
+    assert n == len(ref) and np.array_equal(out, ref)
+    assert st[2] > 0 and st[6] > 0
+    rng = np.random.default_rng(40 + M)
+    for _ in range(4):
+        nleaves = int(rng.integers(2, 120))
+        iz, io, sy, syms = random_tree(rng, nleaves)
+        t = H.Tree(iz, io, sy)
+        if t.info()["maxlen"] > 64:
+            continue
+        text = rng.choice(syms, size=int(rng.integers(1, 200000)), p=rng.dirichlet(np.full(nleaves, 0.3))).astype(np.uint8)
+        data, bits = t.encode(text)
+        for cut in (bits, bits - 1, max(1, bits // 3 + 1)):
+            ref = oracle_chain(iz, io, sy, data, cut)
+            n, out, st, _, _ = run_femu(femu, iz, io, sy, data, cut, M=M)
+            if n == UNSUPPORTED:
+                continue
+            assert n == len(ref) and np.array_equal(out, ref), (cut, st)
 
 
 @pytest.mark.parametrize("seed", range(12))
