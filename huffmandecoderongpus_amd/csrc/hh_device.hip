@@ -2225,9 +2225,15 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
         fsm_stats(d, rg->bits_avail, ro->out_len, ms);
         if (rc == HH_NOSYNC) return HH_ERR_UNSUPPORTED;   // (decode such a code whole)
         // the state leaving a segment does not depend on how it was entered
-        // once the chains have met inside it; the entry after a prologue is
-        // checked against the predecessor's leave state by the caller
-        ro->const_seen = 1;
+        // once the chain from its entry has met an entry-independent one
+        // (a head's).  The count pass proves that meeting only through a
+        // tile's lane-63 walk into its successor (a chain that does not meet
+        // there fails the decode), so only a segment of two or more count
+        // tiles has a leave state proven independent of its entry (the count
+        // pass's tiles: fsm.cm emission tiles each); a one-tile segment's is
+        // valid only when its entry is.  The entry after a prologue is
+        // checked against the predecessor's leave state by the caller.
+        ro->const_seen = rg->ntiles > (uint64_t)d->fsm.cm;
         ro->entry_exact = rg->prologue == 0;
         return rc;
     }
@@ -2354,6 +2360,7 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
     }
     uint64_t total = 0;
     uint32_t state = 0;
+    bool over = false;
     float ms_all[3] = {0, 0, 0};
     for (uint64_t k = 0; k < nch && !rc; k++) {
         const uint64_t b0 = k * ch * 8;
@@ -2367,17 +2374,26 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
         uint64_t n = 0;
         uint32_t leave = 0, en = 0;
         float ms[3] = {0, 0, 0};
+        // (past a capacity failure the later chunks are only counted -- no
+        // room is left, nothing is written -- so that out_len is the stream's
+        // total, as hh_decode_device reports it)
+        const uint64_t room = over || total >= cap ? 0 : cap - total;
         rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, din + k * ch, avail, ntiles, state, 0,
-                        dout + total, cap - total, d->stream, &n, &leave, &en, ms);
+                        room ? dout + total : dout, room, d->stream, &n, &leave, &en, ms);
+        if (rc == HH_ERR_CAPACITY) {
+            over = true;
+            rc = HH_OK;
+        }
         if (rc) break;
         for (int i = 0; i < 3; i++) ms_all[i] += ms[i];
-        if (n && hipMemcpyAsync(out + total, dout + total, n, hipMemcpyDeviceToHost, d->d2h) != hipSuccess) {
+        if (!over && n && hipMemcpyAsync(out + total, dout + total, n, hipMemcpyDeviceToHost, d->d2h) != hipSuccess) {
             rc = HH_ERR_DEVICE;
             break;
         }
         total += n;
         state = leave;
     }
+    if (over && !rc) rc = HH_ERR_CAPACITY;
     if (hipStreamSynchronize(d->d2h) != hipSuccess || hipStreamSynchronize(d->h2d) != hipSuccess) rc = rc ? rc : HH_ERR_DEVICE;
     (void)hipHostUnregister((void *)data);
     if (cap) (void)hipHostUnregister(out);

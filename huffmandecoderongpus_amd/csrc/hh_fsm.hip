@@ -386,7 +386,8 @@ __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns, uint32_t cb) {
 // region's last G bits -- pv, the HB bytes before the tile: uniform words, a
 // chain every lane runs alike (broadcast reads), interleaved with its own
 // head.  Both as rows; hp = hin when given.
-template <uint32_t SW, uint32_t CB>
+// (PV = false: hin is always given, pv never read)
+template <uint32_t SW, uint32_t CB, bool PV = true>
 __device__ __forceinline__ void cnt_heads(const uint8_t *lds, const uint32_t *w, const uint32_t *pv, uint32_t G,
                                           uint32_t hin, uint32_t &gs, uint32_t &hp) {
     constexpr uint32_t S = 32 * SW, RM = CntFmt<CB>::RM;
@@ -398,7 +399,7 @@ __device__ __forceinline__ void cnt_heads(const uint8_t *lds, const uint32_t *w,
     const uint32_t GS = G / CB;                       // (uniform)
     gs = 0;
     hp = 0;
-    if (hin == HIN_NONE) {
+    if (PV && hin == HIN_NONE) {
 #pragma unroll
         for (uint32_t k = NS - HS; k < NS; k++)
             if (k >= NS - GS) {
@@ -703,6 +704,246 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
         hin = TAIL ? HIN_NONE : (uint32_t)__builtin_amdgcn_readfirstlane((int)h63);
     }
     CDIAG_FLUSH(wk.dbg);
+}
+
+// ---------------------------------------------------------------------------
+// k_cntm: the count pass with M consecutive regions per lane.  A count tile
+// is 64 x M regions (M emission tiles); lane j counts regions j M .. j M +
+// M - 1 in order, its chain carried from one region into the next, so a head
+// (16 lookups) guesses only the entry of a lane's first region: a region
+// costs 32 + 16 / M count-table lookups instead of 48.  The head of lane j
+// runs over the last G bits of its own last region and guesses lane j+1's
+// first entry (lane 63's: the next tile's, as in k_cnt).  Where a lane's exit
+// differs from that guess, the lane walks its successor's regions in order
+// -- each region's assumed entry read back from the record its owner wrote,
+// the record rewritten with the true entry and the corrected count -- until
+// the chains meet; a walk that crosses all M regions changes the
+// successor's exit, and the successor walks in the next round.  Tile sums
+// and states per emission tile (64 regions: 64 / M lanes), corrections of
+// the next tile's first regions as in k_cnt.
+// ---------------------------------------------------------------------------
+#ifndef HH_CNT_M
+#define HH_CNT_M 1            // regions per lane of the count pass: 2, 4 (k_cntm) or 1 (k_cnt; HH_CNT_M=n overrides)
+#endif
+
+// Lane j walks lane j+1's regions, q0 the first (want: this lane walks; A:
+// the true state entering them, B0: the entry lane j+1 assumed for its
+// first region, both rows).  Out of line (rare; everything by value, so
+// that the kernel's argument structures stay in scalar registers).
+struct CntmWalk {
+    uint32_t A;          // the true state leaving the last region walked (row)
+    int32_t d;           // the count corrections applied
+    uint32_t met;        // the chains met within the regions
+};
+template <uint32_t SW, uint32_t CB, uint32_t M>
+__device__ __noinline__ CntmWalk cntm_walk(const uint32_t *b1, const uint32_t *__restrict__ g, uint64_t nwords,
+                                           uint32_t *rec, uint64_t q0, bool want, uint32_t A, uint32_t B0) {
+    constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS;
+    bool met = !want;
+    uint32_t a = A, b = B0;
+    int32_t dsum = 0;
+    for (uint32_t r = 0; r < M; r++) {
+        if (__ballot(!met) == 0) break;
+        const uint64_t q = q0 + r;                       // (lane j+1's region r)
+        uint32_t nv[SW], rc = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) nv[k] = 0u;
+        if (!met) {
+            fs_load<SW>(nv, fs_rsrc(g, q * SW, nwords), 0);
+            // the record as it stands (written by its owner, or by this
+            // walk's earlier round): the entry of the chain it counts
+            rc = __hip_atomic_load(&rec[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (r > 0) b = fsm_rec_ent(rc) << RS;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) asm volatile("" : "+v"(nv[k]));
+        uint32_t aa = met ? 0u : a, bb = met ? 0u : b;
+        int32_t dd = 0;
+        walk_region<SW, false, CB>(nullptr, b1, nv, aa, bb, dd, S);
+        if (!met) {
+            rec[q] = fsm_rec(a >> RS, (uint32_t)((int32_t)fsm_rec_cnt(rc) + dd));
+            dsum += dd;
+            met = aa == bb;
+            a = aa;
+        }
+    }
+    return CntmWalk{a, dsum, met ? 1u : 0u};
+}
+
+template <uint32_t SW, uint32_t CB, uint32_t M>
+__global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cntm(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+                                                  uint64_t c0, uint64_t c1) {
+    static_assert((32 * SW) % CB == 0 && 64 % M == 0, "whole count steps per region, lanes in whole emission tiles");
+    extern __shared__ __align__(16) uint8_t smem[];
+    constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS, LG = 64 / M;   // LG: lanes per emission tile
+    constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
+    constexpr uint32_t HWL = HeadGeo<SW, CB>::HWL;
+    const uint32_t ns = geo.ns, tid = threadIdx.x, j = tid & 63u;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    uint32_t *s_b1 = (uint32_t *)(smem + (ns << (CB + 1)));
+    uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
+    for (uint32_t i = tid; i < (ns << (CB - 1)); i += blockDim.x) ((uint32_t *)smem)[i] = ((const uint32_t *)tab.ct)[i];
+    for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
+    for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
+    __syncthreads();
+    const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts, CB};
+    // each wave counts a contiguous run of count tiles, in order (lane 0's
+    // entry guess of a tile: the previous tile's lane-63 head)
+    const uint32_t nwv = gridDim.x * CW, ce = (uint32_t)c1, gw = blockIdx.x * CW + wv;
+    const uint32_t run = ((uint32_t)(c1 - c0) + nwv - 1) / nwv;
+    uint32_t c = (uint32_t)c0 + gw * run;
+    const uint32_t cend = c + run < ce ? c + run : ce;
+    // region words a region ahead (the next tile's first after a tile's
+    // last), the head words (the last region's [HWL, SW)) a tile ahead
+    auto load_region = [&](uint32_t *v, uint32_t cc, uint32_t r, uint32_t a, uint32_t b) {
+        cc = (uint32_t)__builtin_amdgcn_readfirstlane((int)cc);
+        const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, (uint64_t)cc * (64u * M) * SW, geo.nwords);
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        const uint32_t wo = (ln * M + r) * SW;
+        if (SW % 4 == 0 && a % 4 == 0 && b % 4 == 0) {
+#pragma unroll
+            for (uint32_t k = 0; k < SW; k += 4)
+                if (k >= a && k < b) {
+                    const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, 0));
+                    v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
+                }
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < SW; k++)
+                if (k >= a && k < b) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * (wo + k)), 0, 0);
+        }
+    };
+    if (c == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
+    if (c >= cend) return;
+    c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+    uint32_t pw[SW], ph[SW];
+    load_region(pw, c, 0, 0, SW);
+    load_region(ph, c, M - 1, HWL, SW);
+    // the run's first tile: lane 0's entry guess from the HB bytes before it
+    // (later tiles: the previous tile's lane-63 head) -- once, before the loop
+    uint32_t hin = 0;
+    {
+        uint32_t pv[HB / 4];
+        const uint64_t tw = (uint64_t)c * (64u * M) * SW, pa = tw >= HB / 4 ? tw - HB / 4 : 0u;   // (tile 0: unused)
+        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (j % (HB / 4))), 0, 0);
+#pragma unroll
+        for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
+        uint32_t gx = 0;
+        if (geo.G) cnt_heads<SW, CB>(smem, ph, pv, geo.G, HIN_NONE, gx, hin);
+        hin = (uint32_t)__builtin_amdgcn_readfirstlane((int)hin);
+    }
+    __builtin_amdgcn_s_waitcnt(VMCNT0);
+    for (; c < cend; c++) {
+        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+        const uint64_t Q0 = (uint64_t)c * (64u * M);     // the tile's first region
+        const uint32_t cn = c + 1 < cend ? c + 1 : c;
+        const bool has_next = (uint64_t)(c + 1) * M < geo.ntiles;
+        // decodeallbits: lane j's guess for lane j+1's first region, lane 0's
+        // for its own (the previous tile's lane-63 head, or from pv)
+        uint32_t gs = 0, hp = hin;
+        if (geo.G) cnt_heads<SW, CB, false>(smem, ph, nullptr, geo.G, hin, gs, hp);
+        load_region(ph, cn, M - 1, HWL, SW);            // (the next tile's head words)
+        const uint32_t gup = shfl_up1(gs);
+        const uint32_t sp = j ? gup : (c == 0 ? geo.in_state << RS : hp);
+        // the lane's regions in order (records through a buffer resource on
+        // the tile's: a scalar base, a 32-bit lane offset)
+        const __amdgpu_buffer_rsrc_t rrs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(wk.rec + Q0), 0, (int)(64u * M * 4u), 0x00020000);
+        uint32_t s = sp, nsum = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < M; r++) {
+            uint32_t w[SW];
+#pragma unroll
+            for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
+            if (r + 1 < M) load_region(pw, c, r + 1, 0, SW);
+            else load_region(pw, cn, 0, 0, SW);
+            uint32_t n;
+            const uint32_t X = cnt_region<SW, false, CB>(smem, F.b1, w, s, S, &n);
+            __builtin_amdgcn_raw_buffer_store_b32(fsm_rec(s >> RS, n), rrs, (int)(4u * (j * M + r)), 0, 0);
+            nsum += n;
+            s = X;
+        }
+        uint32_t X = s, E = gs;
+        // makebigtable: walks into the successor's regions (lane 63: into the
+        // next tile's region 0, its corrections in fx as in k_cnt)
+        int32_t d = 0, dsum = 0;
+        bool lost = false;
+        for (int round = 0; round < NR; round++) {
+            const bool want = X != E && (j < 63 || has_next);
+            if (__ballot(want) == 0) break;
+            // (the tile's records -- and the last round's rewrites -- reached
+            // memory: walks read them back)
+            __builtin_amdgcn_s_waitcnt(VMCNT0);
+            uint32_t A = X;
+            bool met;
+            if (j < 63) {
+                const CntmWalk cw = cntm_walk<SW, CB, M>(F.b1, g, geo.nwords, wk.rec, Q0 + (uint64_t)(j + 1) * M, want, A, E);
+                A = cw.A;
+                dsum += cw.d;
+                met = cw.met != 0;
+            } else {
+                // lane 63: the next tile's region 0 (its own record not written yet)
+                uint32_t nv[SW];
+#pragma unroll
+                for (uint32_t k = 0; k < SW; k++) nv[k] = 0u;
+                if (want) fs_load<SW>(nv, fs_rsrc(g, (Q0 + 64u * M) * SW, geo.nwords), 0);
+#pragma unroll
+                for (uint32_t k = 0; k < SW; k++) asm volatile("" : "+v"(nv[k]));
+                uint32_t B = want ? E : X;
+                int32_t dd = 0;
+                walk_region<SW, false, CB>(smem, F.b1, nv, A, B, dd, S);
+                if (want) d += dd;
+                met = !want || A == B;
+            }
+            if (want) E = X;
+            bool deep = want && !met;
+            if (j == 63 && deep) {
+                lost = true;
+                deep = false;
+            }
+            const uint32_t dp = shfl_up1(deep ? 1u : 0u), xa = shfl_up1(A);
+            if (j > 0 && dp) X = xa;
+        }
+        // per emission tile (LG lanes): counts with the walks' corrections
+        const uint32_t recv = shfl_up1((uint32_t)dsum);
+        int32_t v = (int32_t)nsum + (j ? (int32_t)recv : 0);
+#pragma unroll
+        for (uint32_t o = LG / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        const uint32_t grp = j / LG;
+        wk.tsum[(uint64_t)c * M + grp] = v;
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63) >> RS;
+        uint32_t fxv = 0, fail = 0;
+        if (has_next) {
+            const bool lst = __builtin_amdgcn_readlane((int)lost, 63) != 0;
+            if (!lst) {
+                const uint32_t E63 = (uint32_t)__builtin_amdgcn_readlane((int)E, 63) >> RS;
+                const int32_t d63 = __builtin_amdgcn_readlane(d, 63);
+                const uint32_t g63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
+                const bool walked = E63 != g63 || d63 != 0;
+                fxv = (j & (FX_W - 1)) == 0 && walked ? fsm_fx(E63, d63) : 0u;
+            } else {
+                uint32_t f[FX_W], ok = 1;
+                const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
+                if (j == 0) ok = cnt_fix_next(&F, g, (Q0 + 64u * M) * S, S, geo.bits, x, h63, f);
+                else
+                    for (int i = 0; i < FX_W; i++) f[i] = 0;
+#pragma unroll
+                for (int i = 0; i < FX_W; i++) {
+                    const uint32_t fv = (uint32_t)__builtin_amdgcn_readlane((int)f[i], 0);
+                    fxv = (j & (FX_W - 1)) == (uint32_t)i ? fv : fxv;
+                }
+                fail = __builtin_amdgcn_readlane((int)ok, 0) ? 0u : 1u;
+            }
+        }
+        // the next tile's first regions' corrections; none for this tile's
+        // emission tiles after its first (lanes 8 .. 8 M - 1)
+        wk.fx[((uint64_t)c + 1) * M * FX_W + (j & (FX_W - 1))] = fxv;
+        if (j < (M - 1) * FX_W) wk.fx[((uint64_t)c * M + 1) * FX_W + j] = 0u;
+        // states leaving the emission tiles (the last one's is the tile's)
+        wk.xs[(uint64_t)c * M + grp] = (grp == M - 1 ? x : 0u) | fail << 31;
+        hin = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1183,6 +1424,15 @@ typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint
 typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t, uint32_t);
 
 #define FSM_SW_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
+// k_cntm for regions of S = 32 sw bits with count steps of cb bits (M =
+// HH_CNT_M regions per lane): the byte-stepped regions of 256 bits, and the
+// 224-bit regions of trees of more than 127 states
+static kcnt_t kcntm_for(uint32_t sw, uint32_t cb, uint32_t m) {
+    if (cb == 8 && sw == 8) return m == 2 ? k_cntm<8, 8, 2> : m == 4 ? k_cntm<8, 8, 4> : nullptr;
+    if (cb == 7 && sw == HH_FSM_S7 / 32)
+        return m == 2 ? k_cntm<HH_FSM_S7 / 32, 7, 2> : m == 4 ? k_cntm<HH_FSM_S7 / 32, 7, 4> : nullptr;
+    return nullptr;
+}
 static kcnt_t kcnt_for(uint32_t sw, bool tail, uint32_t cb) {
     // 7-bit count steps: trees of more than 127 states, 224-bit regions only
     if (cb == 7) return sw == HH_FSM_S7 / 32 ? (tail ? k_cnt<HH_FSM_S7 / 32, true, 7> : k_cnt<HH_FSM_S7 / 32, false, 7>) : nullptr;
@@ -1259,6 +1509,9 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, 
     // the static copy-out (k_emf, SCO) unless HH_EMF_SCO=0; k_emf falls back
     // to the store loop itself for tiles of more than 16 KiB
     fd->sco = !(getenv("HH_EMF_SCO") && atoi(getenv("HH_EMF_SCO")) == 0);
+    // the count pass with HH_CNT_M regions per lane unless HH_CNT_M=1 is set
+    fd->cm = getenv("HH_CNT_M") ? (uint32_t)atoi(getenv("HH_CNT_M")) : (uint32_t)HH_CNT_M;
+    if (fd->cm != 2 && fd->cm != 4) fd->cm = 1;
     // regions of a code whose lengths differ by at most one bit emit nearly
     // the same number of bytes each: lanes' runs start a fixed stride apart
     // and their stores collide in one bank unless the staging is swizzled
@@ -1286,7 +1539,7 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, 
 
 static int fsm_grids(FsmDev *fd) {
     if (fd->grid_c && fd->sized_S == fd->S && fd->sized_ns == fd->ns && fd->sized_K == fd->K && fd->sized_sco == fd->sco &&
-        fd->sized_cb == fd->cb && fd->sized_swz == fd->swz)
+        fd->sized_cb == fd->cb && fd->sized_swz == fd->swz && fd->sized_cm == fd->cm)
         return HH_OK;
     const uint32_t sw = fd->S / 32;
     const kcnt_t kc = kcnt_for(sw, false, fd->cb);
@@ -1299,6 +1552,13 @@ static int fsm_grids(FsmDev *fd) {
     FS_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (pc < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
     fd->grid_c = (uint32_t)(pc * ncu);
+    fd->grid_cm = 0;
+    const kcnt_t km = fd->cm > 1 ? kcntm_for(sw, fd->cb, fd->cm) : nullptr;
+    if (km) {
+        int pm = 0;
+        FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, km, 64 * CW, lds_cnt(fd)));
+        fd->grid_cm = pm > 0 ? (uint32_t)(pm * ncu) : 0u;
+    }
     fd->grid_e = (uint32_t)(pe * ncu);
     fd->sized_S = fd->S;
     fd->sized_ns = fd->ns;
@@ -1306,6 +1566,7 @@ static int fsm_grids(FsmDev *fd) {
     fd->sized_sco = fd->sco;
     fd->sized_swz = fd->swz;
     fd->sized_cb = fd->cb;
+    fd->sized_cm = fd->cm;
     return HH_OK;
 }
 
@@ -1396,8 +1657,19 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
         // beside the main ones measured slower: the cross-stream waits cost
         // more than the overlap saved, 0.155 -> 0.18 ms at 64 MiB.)
         const uint64_t S = fd->S;
-        const uint64_t nc = bits > TB + S ? std::min<uint64_t>((bits - S - 1) / TB, nt) : 0;
-        if (nc) {
+        uint64_t nc = bits > TB + S ? std::min<uint64_t>((bits - S - 1) / TB, nt) : 0;
+        // k_cntm (M regions per lane) over the whole count tiles in [0, nc),
+        // the tiles after them (fewer than M, and the stream's last) by the
+        // TAIL launch
+        const uint64_t nct = fd->grid_cm ? nc / fd->cm : 0;
+        if (nct) {
+            const uint64_t nwg = (nct + CW - 1) / CW;
+            const uint32_t gc = (uint32_t)(nwg < fd->grid_cm ? nwg : fd->grid_cm);
+            hipLaunchKernelGGL(kcntm_for(sw, fd->cb, fd->cm), dim3(gc), dim3(64 * CW), lds_cnt(fd), st, (const uint32_t *)d_data, geo,
+                               tab, wk, (uint64_t)0, nct);
+            FS_OK(hipGetLastError());
+            nc = nct * fd->cm;
+        } else if (nc) {
             const uint64_t nwg = (nc + CW - 1) / CW;
             const uint32_t gc = (uint32_t)(nwg < fd->grid_c ? nwg : fd->grid_c);
             hipLaunchKernelGGL(kcnt_for(sw, false, fd->cb), dim3(gc), dim3(64 * CW), lds_cnt(fd), st, (const uint32_t *)d_data,

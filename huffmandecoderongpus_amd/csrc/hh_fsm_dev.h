@@ -20,6 +20,9 @@ struct FsmDev {
     uint64_t *et, *er;
     // persistent grids (workgroups), sized by the occupancy API for S / ns
     uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K, sized_sco, sized_cb, sized_swz;
+    uint32_t grid_cm;        // k_cntm's grid (0: no k_cntm for this tree / HH_CNT_M=1)
+    uint32_t cm;             // regions per lane of the count pass (k_cntm, 2 or 4; 1: k_cnt only)
+    uint32_t sized_cm;
     uint32_t sco;            // k_emf's static copy-out (the default; HH_EMF_SCO=0: the store loop)
     uint32_t swz;            // k_emf's swizzled staging: codes whose lengths differ by at most 1 bit
     uint64_t *dbg;           // HH_DIAG builds: phase cycles of k_cnt (16 x u64, the decoder's)

@@ -177,7 +177,10 @@ int hh_decoder_stats(const hh_decoder *dec, hh_stats *st);
  * device buffer d_out (cap bytes).  *out_len receives the number of
  * symbols, i.e. the length the reference computes with findmax + 1
  * (findmax.cl:2-8).  Enqueued on `hip_stream` (a hipStream_t, NULL = the
- * default stream); the call returns after the output length is known.    */
+ * default stream); the call returns after the output length is known.
+ * HH_ERR_CAPACITY (the decode needs more than cap bytes): *out_len is still
+ * the stream's full symbol count -- the size to retry with -- here and in
+ * hh_decode_host; the output buffer's content is then unspecified.       */
 int hh_decode_device(hh_decoder *dec, const void *d_data, uint64_t bits,
                      void *d_out, uint64_t cap, uint64_t *out_len,
                      void *hip_stream);
@@ -233,8 +236,11 @@ typedef struct {
 typedef struct {
     uint64_t out_len;        /* symbols written                             */
     uint32_t leave_state;    /* state leaving the last tile                 */
-    uint32_t const_seen;     /* 1: some emitted tile's table is CONST, so   */
-                             /* leave_state does not depend on the entry    */
+    uint32_t const_seen;     /* 1: leave_state does not depend on the entry */
+                             /* (some emitted tile's table is CONST; on the */
+                             /* state machine: the entry's chain was seen   */
+                             /* to meet a head's, i.e. a segment of more    */
+                             /* than one count tile)                        */
     uint32_t entry_state;    /* state entering the first emitted tile       */
     uint32_t entry_exact;    /* 1: the entry state of the first emitted     */
                              /* tile is exact (no prologue, or some         */

@@ -252,6 +252,41 @@ def test_synthetic_full_size(hh, files_dir, src, mib):
         torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("chunk_kb", [None, 2])
+def test_capacity_error_reports_the_total(hh, files_dir, chunk_kb, monkeypatch):
+    """A capacity failure returns HH_ERR_CAPACITY with out_len = the
+    stream's full symbol count (the size to retry with), the same from
+    hh_decode_device and from hh_decode_host, chunk pipeline or not (2 KiB
+    chunks: the capacity runs out in an early chunk, the later ones are
+    counted only)."""
+    import ctypes as C
+    import torch
+    from huffmandecoderongpus_amd import synth
+    if chunk_kb:
+        monkeypatch.setenv("HH_PIPE_CHUNK_KB", str(chunk_kb))
+    hf, text = synth.load_source(files_dir, "kjv.txt")
+    syn = synth.tiled_stream(hf, text, 1 << 20)
+    host = syn.data[: syn.compressed_bytes].cpu().numpy()
+    L = hh.lib()
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(syn.tree)
+        for cap in (syn.decoded_bytes // 3, syn.decoded_bytes - 1):
+            buf = np.zeros(cap, np.uint8)
+            n = C.c_uint64(0)
+            rc = L.hh_decode_host(dec._h, host.ctypes.data, syn.bits, buf.ctypes.data, cap, C.byref(n))
+            assert rc == -5 and n.value == syn.decoded_bytes, (rc, n.value)
+            d_out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+            n = C.c_uint64(0)
+            rc = L.hh_decode_device(dec._h, syn.data.data_ptr(), syn.bits, d_out.data_ptr(), cap, C.byref(n), None)
+            assert rc == -5 and n.value == syn.decoded_bytes, (rc, n.value)
+        # and the decoder is usable afterwards
+        out = dec.decode_host(host, syn.bits, syn.decoded_bytes)
+        assert synth.verify_tiled(torch.from_numpy(out).cuda(), syn)
+    finally:
+        dec.close()
+
+
 @pytest.mark.parametrize("chunk_kb,mib", [(None, 1024), (4096, 64), (2, 1)])
 def test_evaluate_scope_pipeline(hh, files_dir, chunk_kb, mib, monkeypatch):
     """hh_decode_host (the reference's evaluate() scope) uploads the payload

@@ -9,7 +9,7 @@ import os
 import statistics
 import sys
 
-KERNELS = ("k_cnt", "k_fscan1", "k_fscan2", "k_emf", "k_fixed", "k_one")
+KERNELS = ("k_cntm", "k_cnt", "k_fscan1", "k_fscan2", "k_emf", "k_fixed", "k_one")
 per = {}
 for path in glob.glob(os.path.join(sys.argv[1], "**", "*counter_collection.csv"), recursive=True):
     with open(path) as f:
