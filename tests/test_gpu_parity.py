@@ -397,6 +397,82 @@ def test_emission_staging_variants(hh, files_dir, env, monkeypatch):
         dec.close()
 
 
+@pytest.mark.parametrize("m", ["2", "4"])
+def test_count_pass_regions_per_lane(hh, files_dir, m, monkeypatch):
+    """The count pass with m consecutive regions per lane (k_cntm: one head
+    per lane, the walks read back and rewrite the successor lane's records)
+    gives the same bytes as the oracle: the kjv- and E.coli-tiled streams
+    (the latter through the state machine), cut streams of a 40-leaf and of
+    a 256-leaf random tree (7-bit count steps) whose lengths leave partial
+    count tiles to the tail launch, and segments entered after a prologue."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    monkeypatch.setenv("HH_CNT_M", m)           # read when the tree is set
+    for src in ("kjv.txt", "E.coli"):
+        hf, text = synth.load_source(files_dir, src)
+        syn = synth.tiled_stream(hf, text, 16 << 20)
+        dec = hh.Decoder(0, flags=hh.FLAG_NO_FIXED)
+        try:
+            dec.set_tree(syn.tree)
+            out = torch.full((syn.decoded_bytes + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+            n = dec.decode_device(syn.data, syn.bits, out)
+            torch.cuda.synchronize()
+            st = dec.stats()
+            assert st["state_machine"] == 1 and st["exact_fallback"] == 0, (src, st)
+            assert n == syn.decoded_bytes, src
+            assert synth.verify_tiled(out, syn), src
+            assert int(out[n:n + 64].ne(0xAB).sum()) == 0, src
+        finally:
+            dec.close()
+    rng = np.random.default_rng(91)
+    for nleaves, nsym in ((40, 400_000), (256, 300_000)):
+        iz, io, sy, syms = _random_tree(rng, nleaves)
+        p = rng.dirichlet(np.full(nleaves, 0.5))
+        t = hh.Tree(iz, io, sy)
+        text = rng.choice(syms, size=nsym, p=p).astype(np.uint8)
+        data, bits = t.encode(text)
+        dec = hh.Decoder(0)
+        try:
+            dec.set_tree(t)
+            for cut in (bits, bits - 1, bits // 3 + 7, 64 * 256 * 5 + 11):
+                if cut > bits:
+                    continue
+                ref = _oracle(iz, io, sy, data, cut)
+                got = _decode_dev(hh, dec, data, cut, cut + 16)
+                assert dec.stats()["state_machine"] == 1, nleaves
+                assert len(got) == len(ref) and np.array_equal(got, ref), (nleaves, cut)
+        finally:
+            dec.close()
+    # segments: a 4-shard plan of the kjv-tiled stream, each entered after a
+    # prologue of 2 tiles, concatenate to the whole
+    hf, text = synth.load_source(files_dir, "kjv.txt")
+    syn = synth.tiled_stream(hf, text, 4 << 20)
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(syn.tree)
+        whole = torch.zeros(syn.decoded_bytes + 64, dtype=torch.uint8, device="cuda")
+        nw = dec.decode_device(syn.data, syn.bits, whole)
+        tb = dec.tile_bits()
+        nt = (syn.bits + tb - 1) // tb
+        parts, prev_leave = [], 0
+        for r in range(4):
+            t0, t1 = nt * r // 4, nt * (r + 1) // 4
+            pro = min(2, t0)
+            b0 = (t0 - pro) * tb
+            o = torch.zeros(syn.decoded_bytes + 64, dtype=torch.uint8, device="cuda")
+            res = dec.decode_range_ptr(syn.data.data_ptr() + b0 // 8, syn.bits - b0, t1 - t0 + pro, 0,
+                                       o.data_ptr(), o.numel(), 0, prologue=pro)
+            torch.cuda.synchronize()
+            if r:
+                assert res["entry_state"] == prev_leave, r
+            prev_leave = res["leave_state"]
+            parts.append(o[: res["out_len"]])
+        cat = torch.cat(parts)
+        assert cat.numel() == nw and torch.equal(cat, whole[:nw])
+    finally:
+        dec.close()
+
+
 @pytest.mark.parametrize("name", FIXTURES)
 def test_fixture_legacy_pipeline(hh, files_dir, name):
     """Every fixture through round 2's pipeline (HH_FLAG_LEGACY), device
