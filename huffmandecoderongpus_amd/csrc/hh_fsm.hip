@@ -722,8 +722,14 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
 // and states per emission tile (64 regions: 64 / M lanes), corrections of
 // the next tile's first regions as in k_cnt.
 // ---------------------------------------------------------------------------
+// k_cntm's workgroups: cntm_cw(M) waves each, the register budget of
+// cntm_waves(M) waves per SIMD (a lane holds its whole span of M regions:
+// more than k_cnt's 64 VGPRs).  M = 2: 24 waves per CU in 3 workgroups of 8
+// (80 VGPRs); M = 4: 20 in 2 of 10 (96 VGPRs); each workgroup its tables.
+__host__ __device__ constexpr uint32_t cntm_cw(uint32_t m) { return m >= 4 ? 10u : 8u; }
+__host__ __device__ constexpr uint32_t cntm_waves(uint32_t m) { return m >= 4 ? 5u : 6u; }
 #ifndef HH_CNT_M
-#define HH_CNT_M 1            // regions per lane of the count pass: 2, 4 (k_cntm) or 1 (k_cnt; HH_CNT_M=n overrides)
+#define HH_CNT_M 2            // regions per lane of the count pass: 2, 4 (k_cntm) or 1 (k_cnt; HH_CNT_M=n overrides)
 #endif
 
 // Lane j walks lane j+1's regions, q0 the first (want: this lane walks; A:
@@ -771,7 +777,7 @@ __device__ __noinline__ CntmWalk cntm_walk(const uint32_t *b1, const uint32_t *_
 }
 
 template <uint32_t SW, uint32_t CB, uint32_t M>
-__global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cntm(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+__global__ __launch_bounds__(64 * cntm_cw(M)) __attribute__((amdgpu_waves_per_eu(cntm_waves(M), 8))) void k_cntm(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                   uint64_t c0, uint64_t c1) {
     static_assert((32 * SW) % CB == 0 && 64 % M == 0, "whole count steps per region, lanes in whole emission tiles");
     extern __shared__ __align__(16) uint8_t smem[];
@@ -789,7 +795,8 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts, CB};
     // each wave counts a contiguous run of count tiles, in order (lane 0's
     // entry guess of a tile: the previous tile's lane-63 head)
-    const uint32_t nwv = gridDim.x * CW, ce = (uint32_t)c1, gw = blockIdx.x * CW + wv;
+    constexpr uint32_t CWM = cntm_cw(M);
+    const uint32_t nwv = gridDim.x * CWM, ce = (uint32_t)c1, gw = blockIdx.x * CWM + wv;
     const uint32_t run = ((uint32_t)(c1 - c0) + nwv - 1) / nwv;
     uint32_t c = (uint32_t)c0 + gw * run;
     const uint32_t cend = c + run < ce ? c + run : ce;
@@ -817,9 +824,15 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     if (c == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
     if (c >= cend) return;
     c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
-    uint32_t pw[SW], ph[SW];
-    load_region(pw, c, 0, 0, SW);
-    load_region(ph, c, M - 1, HWL, SW);
+    // a lane's M regions are adjacent in memory (M * SW words): loaded in one
+    // burst, so that every cache line is read once and at once -- loaded a
+    // region at a time, the lines of 64 lanes' spans left L1 between their
+    // loads (5x the L2 reads of k_cnt at M = 4).  The heads read the last
+    // region's words from the same burst.  The next tile's burst is issued
+    // when the last region's words are the only ones still in use.
+    uint32_t span[M * SW];
+#pragma unroll
+    for (uint32_t r = 0; r < M; r++) load_region(span + r * SW, c, r, 0, SW);
     // the run's first tile: lane 0's entry guess from the HB bytes before it
     // (later tiles: the previous tile's lane-63 head) -- once, before the loop
     uint32_t hin = 0;
@@ -830,7 +843,7 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
 #pragma unroll
         for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
         uint32_t gx = 0;
-        if (geo.G) cnt_heads<SW, CB>(smem, ph, pv, geo.G, HIN_NONE, gx, hin);
+        if (geo.G) cnt_heads<SW, CB>(smem, span + (M - 1) * SW, pv, geo.G, HIN_NONE, gx, hin);
         hin = (uint32_t)__builtin_amdgcn_readfirstlane((int)hin);
     }
     __builtin_amdgcn_s_waitcnt(VMCNT0);
@@ -842,8 +855,7 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
         // decodeallbits: lane j's guess for lane j+1's first region, lane 0's
         // for its own (the previous tile's lane-63 head, or from pv)
         uint32_t gs = 0, hp = hin;
-        if (geo.G) cnt_heads<SW, CB, false>(smem, ph, nullptr, geo.G, hin, gs, hp);
-        load_region(ph, cn, M - 1, HWL, SW);            // (the next tile's head words)
+        if (geo.G) cnt_heads<SW, CB, false>(smem, span + (M - 1) * SW, nullptr, geo.G, hin, gs, hp);
         const uint32_t gup = shfl_up1(gs);
         const uint32_t sp = j ? gup : (c == 0 ? geo.in_state << RS : hp);
         // the lane's regions in order (records through a buffer resource on
@@ -855,9 +867,11 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
         for (uint32_t r = 0; r < M; r++) {
             uint32_t w[SW];
 #pragma unroll
-            for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
-            if (r + 1 < M) load_region(pw, c, r + 1, 0, SW);
-            else load_region(pw, cn, 0, 0, SW);
+            for (uint32_t k = 0; k < SW; k++) w[k] = span[r * SW + k];
+            if (r + 1 == M) {
+#pragma unroll
+                for (uint32_t q = 0; q < M; q++) load_region(span + q * SW, cn, q, 0, SW);   // (the next tile's burst)
+            }
             uint32_t n;
             const uint32_t X = cnt_region<SW, false, CB>(smem, F.b1, w, s, S, &n);
             __builtin_amdgcn_raw_buffer_store_b32(fsm_rec(s >> RS, n), rrs, (int)(4u * (j * M + r)), 0, 0);
@@ -1556,7 +1570,7 @@ static int fsm_grids(FsmDev *fd) {
     const kcnt_t km = fd->cm > 1 ? kcntm_for(sw, fd->cb, fd->cm) : nullptr;
     if (km) {
         int pm = 0;
-        FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, km, 64 * CW, lds_cnt(fd)));
+        FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, km, 64 * cntm_cw(fd->cm), lds_cnt(fd)));
         fd->grid_cm = pm > 0 ? (uint32_t)(pm * ncu) : 0u;
     }
     fd->grid_e = (uint32_t)(pe * ncu);
@@ -1663,9 +1677,10 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
         // TAIL launch
         const uint64_t nct = fd->grid_cm ? nc / fd->cm : 0;
         if (nct) {
-            const uint64_t nwg = (nct + CW - 1) / CW;
+            const uint32_t cwm = cntm_cw(fd->cm);
+            const uint64_t nwg = (nct + cwm - 1) / cwm;
             const uint32_t gc = (uint32_t)(nwg < fd->grid_cm ? nwg : fd->grid_cm);
-            hipLaunchKernelGGL(kcntm_for(sw, fd->cb, fd->cm), dim3(gc), dim3(64 * CW), lds_cnt(fd), st, (const uint32_t *)d_data, geo,
+            hipLaunchKernelGGL(kcntm_for(sw, fd->cb, fd->cm), dim3(gc), dim3(64 * cwm), lds_cnt(fd), st, (const uint32_t *)d_data, geo,
                                tab, wk, (uint64_t)0, nct);
             FS_OK(hipGetLastError());
             nc = nct * fd->cm;

@@ -3,7 +3,7 @@ the library named by HIPHUFF_LIB (default: the in-tree build); prints one
 JSON line with the median device time of each kernel phase over N runs and
 whether the output matched the tiled text.
 
-    python tools/time_lib.py [MiB] [runs] [source]   (source: kjv.txt | E.coli)
+    python tools/time_lib.py [MiB] [runs] [source]   (source: kjv.txt | E.coli | bytes)
 """
 import json
 import os
@@ -22,7 +22,11 @@ src = sys.argv[3] if len(sys.argv) > 3 else "kjv.txt"
 # the source text comes from the in-tree library (the A/B scripts cache it), so
 # that an experiment variant under test never decodes its own reference
 cache = os.environ.get("HH_TEXT_CACHE")
-if cache and os.path.exists(cache):
+if src == "bytes":
+    # bench's byte-alphabet workload: generated and encoded on the GPU,
+    # checked against its symbols (no text to cache)
+    hf = text = None
+elif cache and os.path.exists(cache):
     import numpy as np
     hf = H.HuffFile.load(os.path.join(ROOT, "files", src + ".huff"))
     text = np.load(cache)
@@ -32,7 +36,16 @@ else:
         import numpy as np
         np.save(cache, text)
         sys.exit(0)
-syn = synth.tiled_stream(hf, text, mib << 20)
+if src == "bytes":
+    syn = synth.byte_stream(mib << 20)
+else:
+    syn = synth.tiled_stream(hf, text, mib << 20)
+
+
+def verify(out, n):
+    if hf is None:
+        return n == syn.decoded_bytes and bool(torch.equal(out[:n], syn.syms))
+    return n == syn.decoded_bytes and synth.verify_tiled(out, syn)
 dec = H.Decoder(0, lane_bits=int(os.environ.get("HH_LANE_BITS", "0")), flags=int(os.environ.get("HH_FLAGS", "0")))
 dec.set_tree(syn.tree)
 out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device="cuda")
@@ -50,7 +63,7 @@ for i in range(reps + 1):
     torch.cuda.synchronize()
     wall.append((time.perf_counter() - t0) * 1e3)
     if i == 0:
-        ok = n == syn.decoded_bytes and synth.verify_tiled(out, syn)
+        ok = verify(out, n)
         continue
     st = dec.stats()
     for k in ph:
