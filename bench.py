@@ -170,8 +170,27 @@ def cpu_baseline_tiled(H, hf, text, mib: int, jumpbits: int, reps: int, procs: i
                                      f"last one's end; host cores: {os.cpu_count()} visible")}}
 
 
+def phase_split(device: int, tree, flags: int, data, bits: int, out, n: int = 3) -> dict:
+    """Count / scan / emission device times from a separate decoder with
+    HH_FLAG_PHASE_TIMING (events between the kernels, ~6 us of idle GPU
+    each: never in the timed decodes), after the timed region."""
+    import torch
+    d = H.Decoder(device, flags=flags | H.FLAG_PHASE_TIMING)
+    try:
+        d.set_tree(tree)
+        d.decode_device(data, bits, out)
+        st = []
+        for _ in range(n):
+            d.decode_device(data, bits, out)
+            st.append(d.stats())
+        torch.cuda.synchronize()
+    finally:
+        d.close()
+    return {k: round(statistics.mean(s[f"ms_{k}"] for s in st), 4) for k in ("sync", "scan", "emit", "total")}
+
+
 def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, steps: int,
-                    warmup: int) -> dict:
+                    warmup: int, tree=None, flags: int = 0, device: int = 0) -> dict:
     """One more single-GPU workload, device-resident like the headline one:
     correctness first, then `steps` timed decodes as a stream of
     asynchronous decodes (kernel time from the decoder's HIP events, wall
@@ -197,10 +216,10 @@ def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, s
     ms_dev = statistics.mean(s["ms_total"] for s in st)
     C = (bits + 7) // 8
     ach = (C + n_want) / (ms_dev * 1e-3) / 1e9
+    ph = phase_split(device, tree, flags, data, bits, out) if tree is not None else None
     return {"workload": name, "ok": bool(ok), "value": round(n_want / (ms_step * 1e-3) / 1e6, 1),
             "unit": "MB/s", "ms_per_step": round(ms_step, 4), "ms_kernel": round(ms_dev, 4),
-            "ms_front": round(statistics.mean(s["ms_sync"] for s in st), 4),
-            "ms_emit": round(statistics.mean(s["ms_emit"] for s in st), 4),
+            "ms_front": ph["sync"] if ph else None, "ms_emit": ph["emit"] if ph else None,
             "compressed_bytes": C, "decoded_bytes": n_want,
             "roofline_frac": round(ach / HBM_PEAK_GBS, 4),
             "fast_path": all(s["exact_fallback"] == 0 for s in st),
@@ -398,8 +417,9 @@ def main():
 
     ms_step = elapsed / a.steps * 1e3
     ms_dev = statistics.mean(s["ms_total"] for s in dev_ms)
-    phases = {k: round(statistics.mean(s[f"ms_{k}"] for s in dev_ms), 4)
-              for k in ("sync", "scan", "emit")}
+    # the split by kernel from a separate phase-timed decoder (world 1)
+    phases = (phase_split(local, syn.tree, 0, syn.data, syn.bits, out) if world == 1
+              else {"sync": None, "scan": None, "emit": None})
     fast = all(s["exact_fallback"] == 0 for s in dev_ms)
     kernels = ("k_cnt+k_fscan1+k_fscan2+k_emf" if all(s["state_machine"] for s in dev_ms)
                else "k_front+k_walk+k_table+k_scan1+k_scan2+k_emit")
@@ -463,7 +483,7 @@ def main():
         out_e = torch.empty(syn_e.decoded_bytes + 4096, dtype=torch.uint8, device=dev)
         more.append(device_workload(f"synthetic {a.size_mib} MiB E.coli-tiled .huff", dec_e,
                                     syn_e.data, syn_e.bits, out_e, syn_e.decoded_bytes,
-                                    lambda o: synth.verify_tiled(o, syn_e), ks, 2))
+                                    lambda o: synth.verify_tiled(o, syn_e), ks, 2, syn_e.tree, 0, local))
         dec_e.close()
         # the same stream through the general pipeline (heads, exit merges,
         # walks, tables, scans, emission): config 5's merge-density stress
@@ -471,7 +491,8 @@ def main():
         dec_g.set_tree(syn_e.tree)
         more.append(device_workload(f"synthetic {a.size_mib} MiB E.coli-tiled .huff, general pipeline "
                                     f"(HH_FLAG_NO_FIXED)", dec_g, syn_e.data, syn_e.bits, out_e,
-                                    syn_e.decoded_bytes, lambda o: synth.verify_tiled(o, syn_e), ks, 2))
+                                    syn_e.decoded_bytes, lambda o: synth.verify_tiled(o, syn_e), ks, 2,
+                                    syn_e.tree, H.FLAG_NO_FIXED, local))
         dec_g.close()
         del out_e, syn_e
         torch.cuda.empty_cache()
@@ -481,7 +502,7 @@ def main():
                                     f"(splitmix64 seed {synth.IID_SEED:#x})", dec, iid.data,
                                     iid.bits, out_i, iid.decoded_bytes,
                                     lambda o: bool(torch.equal(o[:iid.decoded_bytes], iid.syms)),
-                                    ks, 2))
+                                    ks, 2, iid.tree, 0, local))
         del out_i, iid
         torch.cuda.empty_cache()
         # a byte alphabet: Huffman code over all 256 byte values (255 states,
@@ -494,7 +515,8 @@ def main():
                                     f"code, Zipf s={synth.ZIPF_S} byte frequencies, splitmix64 seed "
                                     f"{synth.BYTE_SEED:#x})", dec_b, byt.data, byt.bits, out_b,
                                     byt.decoded_bytes,
-                                    lambda o: bool(torch.equal(o[:byt.decoded_bytes], byt.syms)), ks, 2))
+                                    lambda o: bool(torch.equal(o[:byt.decoded_bytes], byt.syms)), ks, 2,
+                                    byt.tree, 0, local))
         dec_b.close()
         del out_b, byt
         torch.cuda.empty_cache()

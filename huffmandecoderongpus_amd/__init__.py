@@ -81,6 +81,7 @@ FLAG_FORCE_EXACT = 1
 FLAG_FORCE_SEGMENT = 2
 FLAG_NO_FIXED = 4     # HH_FLAG_NO_FIXED: fixed-length codes through the general pipeline too
 FLAG_LEGACY = 8       # HH_FLAG_LEGACY: round 2's pipeline instead of the state-machine decode
+FLAG_PHASE_TIMING = 16  # HH_FLAG_PHASE_TIMING: events between the kernels (ms_sync/scan/emit)
 _lib_handle: Optional[C.CDLL] = None
 
 # exported symbols and their ctypes signatures; tests check every one of these

@@ -1605,9 +1605,8 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     // the state machine (trees of at most HH_FSM_MAXS = 255 internal nodes)
     fsm_free(&d->fsm);
     // emission steps of 7 bits when their tables leave room for 16 stagings
-    // of the expected tile output (fsm_k_fits), else 6 (smaller tables, more
-    // waves: E.coli-like codes of 2 bits fill 8 KiB per tile); HH_FSM_K:
-    // experiments.  Expected bits per symbol: the code lengths weighted by
+    // of the expected tile output (fsm_k_fits), else 6 or 5 (smaller tables,
+    // more waves), 6 when none does; HH_FSM_K: experiments.  Expected bits per symbol: the code lengths weighted by
     // 2^-length (exact for a code built from a dyadic distribution).
     double avg = 0.0;
     {
@@ -1623,13 +1622,18 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
     }
     const uint32_t est = avg > 0.0 ? (uint32_t)(64.0 * d->S / avg) : 64u * d->S;
     uint32_t Kf = getenv("HH_FSM_K") ? (uint32_t)atoi(getenv("HH_FSM_K")) : 0u;
-    if (!Kf && d->S && hh_fsm_build(d->ht, d->S, 7, d->ft) == HH_OK && fsm_k_fits(d->ft, est)) Kf = 7;
+    // the widest step whose tables leave room for 16 stagings: kjv-like
+    // alphabets 7; a byte alphabet (255 states, at most 6) 5 -- its 6-bit
+    // tables leave room for 6 waves' stagings (emit 1.07 -> 0.97 ms per GiB)
+    for (uint32_t k = 7; !Kf && d->S && k >= 5; k--)
+        if (hh_fsm_build(d->ht, d->S, k, d->ft) == HH_OK && d->ft->K == k && fsm_k_fits(d->ft, est)) Kf = k;
     if (d->S && hh_fsm_build(d->ht, d->S, Kf ? Kf : 6, d->ft) == HH_OK) {
         uint32_t Gf = hh_fsm_pick_head(d->ht, d->S, d->ft->cb);
         if (getenv("HH_FSM_HEAD")) Gf = (uint32_t)atoi(getenv("HH_FSM_HEAD")) / d->ft->cb * d->ft->cb;   // experiments
         if (Gf > d->S) Gf = 0;
         const int urc = fsm_upload(&d->fsm, d->ft, Gf, (uint32_t)d->ht->minlen, (uint32_t)d->ht->maxlen);
         d->fsm.dbg = d->d_dbg;
+        d->fsm.phases = (d->cfg.flags & HH_FLAG_PHASE_TIMING) != 0;
         if (urc != HH_OK && urc != HH_ERR_UNSUPPORTED) return urc;
     }
     d->have_tree = 1;
@@ -2023,11 +2027,12 @@ static int fixed_path(hh_decoder *d, const void *d_data, uint64_t bits, uint8_t 
 static bool fsm_path_ok(const hh_decoder *d) {
     return d->fsm.ok && !(d->cfg.flags & (HH_FLAG_LEGACY | HH_FLAG_FORCE_EXACT | HH_FLAG_FORCE_SEGMENT));
 }
+// ms: count, scan, emission (HH_FLAG_PHASE_TIMING; else 0), total
 static void fsm_stats(hh_decoder *d, uint64_t bits, uint64_t total, const float *ms) {
     d->stats.ms_sync = ms[0];
     d->stats.ms_scan = ms[1];
     d->stats.ms_emit = ms[2];
-    d->stats.ms_total = ms[0] + ms[1] + ms[2];
+    d->stats.ms_total = ms[3];
     d->stats.lanes = (bits + d->S - 1) / d->S;
     d->stats.out_len = total;
     d->stats.state_machine = 1;
@@ -2052,7 +2057,7 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
     if (fsm_path_ok(d)) {
         uint64_t total = 0;
         uint32_t leave = 0, en = 0;
-        float ms[3] = {0, 0, 0};
+        float ms[4] = {0, 0, 0, 0};
         const int rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, d_data, bits, 0, 0, 0, d_out, cap, st,
                                   &total, &leave, &en, ms);
         fsm_stats(d, bits, total, ms);
@@ -2120,7 +2125,7 @@ static int async_check(hh_decoder *d) {
     } else {
         uint64_t total = 0;
         uint32_t leave = 0, en = 0;
-        float ms[3] = {0, 0, 0};
+        float ms[4] = {0, 0, 0, 0};
         rc = fsm_collect(&d->fsm_ws, ev, &d->apend.pd, &total, &leave, &en, ms);
         fsm_stats(d, d->apend.bits, total, ms);
         *d->apend.out_len = total;
@@ -2218,7 +2223,7 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
     if (fsm_path_ok(d)) {
         // states are state-machine states (0: the root, the stream start)
         if (rg->in_state >= d->fsm.ns) return HH_ERR_ARG;
-        float ms[3] = {0, 0, 0};
+        float ms[4] = {0, 0, 0, 0};
         const int rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, d_data, rg->bits_avail, rg->ntiles,
                                   rg->in_state, rg->prologue, d_out, cap, st, &ro->out_len, &ro->leave_state,
                                   &ro->entry_state, ms);
@@ -2361,7 +2366,7 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
     uint64_t total = 0;
     uint32_t state = 0;
     bool over = false;
-    float ms_all[3] = {0, 0, 0};
+    float ms_all[4] = {0, 0, 0, 0};
     for (uint64_t k = 0; k < nch && !rc; k++) {
         const uint64_t b0 = k * ch * 8;
         const uint64_t ntiles = (k + 1 < nch ? ch * 8 : bits - b0 + d->S * HH_NR - 1) / (d->S * HH_NR);
@@ -2373,7 +2378,7 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
         // kernels read it only for chains that this segment does not use)
         uint64_t n = 0;
         uint32_t leave = 0, en = 0;
-        float ms[3] = {0, 0, 0};
+        float ms[4] = {0, 0, 0, 0};
         // (past a capacity failure the later chunks are only counted -- no
         // room is left, nothing is written -- so that out_len is the stream's
         // total, as hh_decode_device reports it)
@@ -2385,7 +2390,7 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
             rc = HH_OK;
         }
         if (rc) break;
-        for (int i = 0; i < 3; i++) ms_all[i] += ms[i];
+        for (int i = 0; i < 4; i++) ms_all[i] += ms[i];
         if (!over && n && hipMemcpyAsync(out + total, dout + total, n, hipMemcpyDeviceToHost, d->d2h) != hipSuccess) {
             rc = HH_ERR_DEVICE;
             break;

@@ -34,7 +34,7 @@
  *                     stream (its tail rule, decodeallbits.cl:20-31)
  *   et[s << K | v]    u64: K-bit steps (emission), v = the next K bits
  *       bits  0..31   the symbols completed (first in bits 0..7, unused
- *                     bytes 0): K = 6 or 7 for codes of >= 2 bits, K = 4
+ *                     bytes 0): K = 4..7 for codes of >= 2 bits, K = 4
  *                     when a code has 1 bit; a step from inside a code
  *                     completes up to 3 (K = 6) or 4 (K = 7, 4) symbols
  *       bits 32..39   8 x the number of symbols (the output shift)
@@ -78,7 +78,7 @@ typedef struct {
 extern "C" {
 #endif
 /* Builds the state machine of the compact tree in T (hh_tables_build) for
- * regions of S bits, emission steps of K bits (6 or 7; 0: 6; a code of 1 bit
+ * regions of S bits, emission steps of K bits (4..7; 0: 6; a code of 1 bit
  * takes K = 4 whatever is asked; trees of more than HH_FSM_MAXS8 internal
  * nodes take at most 6).  Count steps of 8 bits when ns <= HH_FSM_MAXS8 and
  * S is whole bytes, else of 7 bits (S a multiple of 7).  HH_ERR_UNSUPPORTED

@@ -77,6 +77,26 @@ static_assert(FX_W == HH_FSM_KM, "corrections per tile");
 enum { FF_FAIL = 1, FF_OVER = 2 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// A table into LDS at a workgroup's start: 16-B loads, UNR of them in flight
+// per thread before their stores (a loop of 4-B load -> store pairs waited
+// for each load in turn: ~20 round trips to L2 per 42 KB table).  bytes: a
+// multiple of 16; dst and src 16-B aligned.
+template <uint32_t UNR = 4>
+__device__ __forceinline__ void lds_fill16(uint8_t *dst, const void *src, uint32_t bytes) {
+    const u32x4 *s = (const u32x4 *)src;
+    u32x4 *d = (u32x4 *)dst;
+    const uint32_t n = bytes / 16u, step = blockDim.x;
+    for (uint32_t i = threadIdx.x; i < n; i += UNR * step) {
+        u32x4 v[UNR];
+#pragma unroll
+        for (uint32_t u = 0; u < UNR; u++)
+            if (i + u * step < n) v[u] = __builtin_nontemporal_load(s + i + u * step);
+#pragma unroll
+        for (uint32_t u = 0; u < UNR; u++)
+            if (i + u * step < n) d[i + u * step] = v[u];
+    }
+}
 typedef uint32_t u32u __attribute__((aligned(1)));   // an LDS word at any byte address
 
 struct FsmGeo {
@@ -569,9 +589,12 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
 #ifndef HH_CNT_WAVES
 #define HH_CNT_WAVES 8        // k_cnt: waves per SIMD the register budget is cut for (32 per CU: 2 workgroups of 16)
 #endif
-template <uint32_t SW, bool TAIL, uint32_t CB>
-__global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
-                                                 uint64_t t0, uint64_t t1) {
+// The count pass over tiles [t0, t1) as workgroup blk of nblk with CWX waves
+// each (k_cnt; and the tail tiles run by the last workgroups of k_cntm's
+// launch, instead of a launch of their own after it).
+template <uint32_t SW, bool TAIL, uint32_t CB, uint32_t CWX>
+__device__ __forceinline__ void cnt_run(const uint32_t *__restrict__ g, const FsmGeo &geo, const FsmTab &tab,
+                                        const FsmWork &wk, uint64_t t0, uint64_t t1, uint32_t blk, uint32_t nblk) {
     static_assert((32 * SW) % CB == 0, "whole count steps per region");
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW;
@@ -579,7 +602,7 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // (uniform: scalar tile index)
     uint32_t *s_b1 = (uint32_t *)(smem + (ns << (CB + 1)));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
-    for (uint32_t i = tid; i < (ns << (CB - 1)); i += blockDim.x) ((uint32_t *)smem)[i] = ((const uint32_t *)tab.ct)[i];
+    lds_fill16(smem, tab.ct, ns << (CB + 1));            // (ns x 2^CB u16: a multiple of 16 B)
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
     __syncthreads();
@@ -590,7 +613,7 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     // each wave counts a contiguous run of tiles, in order (TAIL launches: a
     // tile per wave): lane 0's region-0 guess of a tile is then the previous
     // tile's lane-63 head, so only a run's first tile computes it
-    const uint32_t nwv = gridDim.x * CW, te = (uint32_t)t1, gw = blockIdx.x * CW + wv;
+    const uint32_t nwv = nblk * CWX, te = (uint32_t)t1, gw = blk * CWX + wv;
     const uint32_t run = TAIL ? 1u : ((uint32_t)(t1 - t0) + nwv - 1) / nwv;
     uint32_t t = TAIL ? (uint32_t)t0 + gw : (uint32_t)t0 + gw * run;
     const uint32_t tend = TAIL ? te : (t + run < te ? t + run : te);
@@ -706,6 +729,12 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
     CDIAG_FLUSH(wk.dbg);
 }
 
+template <uint32_t SW, bool TAIL, uint32_t CB>
+__global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+                                                 uint64_t t0, uint64_t t1) {
+    cnt_run<SW, TAIL, CB, CW>(g, geo, tab, wk, t0, t1, blockIdx.x, gridDim.x);
+}
+
 // ---------------------------------------------------------------------------
 // k_cntm: the count pass with M consecutive regions per lane.  A count tile
 // is 64 x M regions (M emission tiles); lane j counts regions j M .. j M +
@@ -778,8 +807,17 @@ __device__ __noinline__ CntmWalk cntm_walk(const uint32_t *b1, const uint32_t *_
 
 template <uint32_t SW, uint32_t CB, uint32_t M>
 __global__ __launch_bounds__(64 * cntm_cw(M)) __attribute__((amdgpu_waves_per_eu(cntm_waves(M), 8))) void k_cntm(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
-                                                  uint64_t c0, uint64_t c1) {
+                                                  uint64_t c0, uint64_t c1, uint64_t u0, uint64_t u1, uint32_t ntb) {
     static_assert((32 * SW) % CB == 0 && 64 % M == 0, "whole count steps per region, lanes in whole emission tiles");
+    constexpr uint32_t CWM = cntm_cw(M);
+    // the first ntb workgroups (dispatched first, resident beside the rest):
+    // the emission tiles [u0, u1) after the count tiles, one per wave with
+    // the stream-end checks (TAIL) -- a launch of their own after this one
+    // cost a tile's time at the end of every decode
+    if (blockIdx.x < ntb) {
+        cnt_run<SW, true, CB, CWM>(g, geo, tab, wk, u0, u1, blockIdx.x, ntb);
+        return;
+    }
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS, LG = 64 / M;   // LG: lanes per emission tile
     constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
@@ -788,15 +826,14 @@ __global__ __launch_bounds__(64 * cntm_cw(M)) __attribute__((amdgpu_waves_per_eu
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     uint32_t *s_b1 = (uint32_t *)(smem + (ns << (CB + 1)));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
-    for (uint32_t i = tid; i < (ns << (CB - 1)); i += blockDim.x) ((uint32_t *)smem)[i] = ((const uint32_t *)tab.ct)[i];
+    lds_fill16(smem, tab.ct, ns << (CB + 1));            // (ns x 2^CB u16: a multiple of 16 B)
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
     __syncthreads();
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts, CB};
     // each wave counts a contiguous run of count tiles, in order (lane 0's
     // entry guess of a tile: the previous tile's lane-63 head)
-    constexpr uint32_t CWM = cntm_cw(M);
-    const uint32_t nwv = gridDim.x * CWM, ce = (uint32_t)c1, gw = blockIdx.x * CWM + wv;
+    const uint32_t nwv = (gridDim.x - ntb) * CWM, ce = (uint32_t)c1, gw = (blockIdx.x - ntb) * CWM + wv;
     const uint32_t run = ((uint32_t)(c1 - c0) + nwv - 1) / nwv;
     uint32_t c = (uint32_t)c0 + gw * run;
     const uint32_t cend = c + run < ce ? c + run : ce;
@@ -1117,8 +1154,9 @@ struct EmfChain {
         const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
         const uint32_t u = sh + (hi & 255u);          // 8 x the symbols: one SDWA add
         // the bytes that do not fit the current dword spill into the next;
-        // K = 6 steps carry at most 3 symbols, so nothing spills at sh = 0,
-        // K = 7 and K = 4 steps up to 4 (7 bits from inside a code: 1 + 3 x 2)
+        // K = 6 (and 5) steps carry at most 3 symbols, so nothing spills at
+        // sh = 0, K = 7 and K = 4 steps up to 4 (7 bits from inside a code:
+        // 1 + 3 x 2; 4 bits of 1-bit codes)
         const uint32_t an = (lo << sh) | a;
         uint32_t sp = __builtin_amdgcn_alignbit(0u, lo, (0u - sh) & 31u);
         if (K != 6) sp = sh ? sp : 0u;
@@ -1256,10 +1294,12 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
 // compiler waits vmcnt(0) at every tile's start (30 % of the kernel's wave
 // cycles in the HH_DIAG build).  (Round 3 measured a fixed COI of 16 no
 // faster: three quarters of its stores were empty.)
-template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO, bool SWZ = false>
-__global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
-                                                 uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1,
-                                                 uint32_t lds_bytes) {
+// The emission of tiles [t0, t1) as workgroup blk of nblk (k_emf; and the
+// tail tiles run by k_emf's first workgroups).
+template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO, bool SWZ>
+__device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const FsmGeo &geo, const FsmTab &tab,
+                                        const FsmWork &wk, uint8_t *__restrict__ out, uint64_t cap, uint64_t t0,
+                                        uint64_t t1, uint32_t lds_bytes, uint32_t blk, uint32_t nblk) {
     static_assert(!TAIL || NCH == 1, "the tail tiles take one chain per lane");
     static_assert(!SWZ || !TAIL, "the tail tiles' staging is not swizzled");
     extern __shared__ __align__(16) uint8_t smem[];
@@ -1270,7 +1310,7 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
     uint32_t *s_b1 = (uint32_t *)(smem + er_off + (r ? (ns << r) * 8u : 0u));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
     constexpr uint32_t EW = emf_waves(NCH);
-    for (uint32_t i = tid; i < (ns << K); i += blockDim.x) ((uint64_t *)smem)[i] = tab.et[i];
+    lds_fill16(smem, tab.et, (ns << K) * 8u);             // (ns x 2^K u64: a multiple of 16 B)
     for (uint32_t i = tid; r && i < (ns << r); i += blockDim.x) ((uint64_t *)(smem + er_off))[i] = tab.er[i];
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
@@ -1292,7 +1332,7 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
     // compile-time count: see above) or (COI = 0) a loop over the tile's bytes
     auto tiles = [&](auto coi) {
     constexpr uint32_t COI = decltype(coi)::value;
-        const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)gridDim.x * nact;
+        const uint64_t TB = (uint64_t)NR * S, nwv = (uint64_t)nblk * nact;
         // next tiles' words, records, corrections and bases, loaded one step
         // ahead (the base words by lanes 0..2, read out with readlane where consumed)
         uint32_t pw[NCH][SW], prec[NCH], pfx[NCH], pmeta[NCH];
@@ -1310,7 +1350,7 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
                 fs_load<SW>(pw[c], rs, j * SW);
             }
         };
-        uint64_t t = t0 + (uint64_t)blockIdx.x * nact + wv;
+        uint64_t t = t0 + (uint64_t)blk * nact + wv;
         EDIAG_DECL
         if (t < t1) prefetch(t);
         // (the first tile's loads complete here, once per wave: the compiler
@@ -1431,17 +1471,34 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
     EDIAG_FLUSH(wk.dbg);
 }
 
+// k_emf: the emission of tiles [t0, t1); its first ntb workgroups (dispatched
+// first, resident beside the rest) emit the stream's last tiles [u0, u1)
+// with the stream-end checks (TAIL) -- a launch of their own after this one
+// cost a tile's time at the end of every decode.
+template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO, bool SWZ = false>
+__global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+                                                 uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1,
+                                                 uint32_t lds_bytes, uint64_t u0, uint64_t u1, uint32_t ntb) {
+    if (!TAIL && blockIdx.x < ntb) {
+        emf_run<SW, K, true, 1, false, false>(g, geo, tab, wk, out, cap, u0, u1, lds_bytes, blockIdx.x, ntb);
+        return;
+    }
+    emf_run<SW, K, TAIL, NCH, SCO, SWZ>(g, geo, tab, wk, out, cap, t0, t1, lds_bytes, blockIdx.x - ntb, gridDim.x - ntb);
+}
+
 // ---------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------
 typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint64_t);
-typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t, uint32_t);
+typedef void (*kcntm_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t);
+typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t, uint32_t, uint64_t,
+                       uint64_t, uint32_t);
 
 #define FSM_SW_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
 // k_cntm for regions of S = 32 sw bits with count steps of cb bits (M =
 // HH_CNT_M regions per lane): the byte-stepped regions of 256 bits, and the
 // 224-bit regions of trees of more than 127 states
-static kcnt_t kcntm_for(uint32_t sw, uint32_t cb, uint32_t m) {
+static kcntm_t kcntm_for(uint32_t sw, uint32_t cb, uint32_t m) {
     if (cb == 8 && sw == 8) return m == 2 ? k_cntm<8, 8, 2> : m == 4 ? k_cntm<8, 8, 4> : nullptr;
     if (cb == 7 && sw == HH_FSM_S7 / 32)
         return m == 2 ? k_cntm<HH_FSM_S7 / 32, 7, 2> : m == 4 ? k_cntm<HH_FSM_S7 / 32, 7, 4> : nullptr;
@@ -1469,7 +1526,7 @@ static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sc
                                         : sco ? k_emf<n, k, false, 1, true> : k_emf<n, k, false, 1, false>)
 #define X(n)                                                                            \
     case n:                                                                             \
-        return K == 7 ? EMF_K(n, 7) : K == 6 ? EMF_K(n, 6) : K == 4 ? EMF_K(n, 4) : nullptr;
+        return K == 7 ? EMF_K(n, 7) : K == 6 ? EMF_K(n, 6) : K == 5 ? EMF_K(n, 5) : K == 4 ? EMF_K(n, 4) : nullptr;
         FSM_SW_CASES(X)
 #undef X
 #undef EMF_K
@@ -1484,11 +1541,11 @@ static size_t lds_cnt(const FsmDev *fd) { return cnt_tab_bytes(fd->ns, fd->cb); 
 static size_t lds_emf(const FsmDev *) { return EMF_LDS; }
 static_assert(EMF_LDS <= 160u * 1024u, "k_emf's LDS");
 
-// 7-bit emission steps when their tables leave room for 16 stagings of the
-// expected tile output
+// the emission tables of F leave room for 16 stagings of the expected tile
+// output (k_emf sizes them at run time)
 bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile) {
-    const uint64_t need = ((uint64_t)est_tile + 16u + 8u + 15u) & ~15ull;   // (the stagings are sized at run time)
-    return F->K == 7 && emf_tab_bytes(F->ns, 7, F->r) + 16u * need <= EMF_LDS;
+    const uint64_t need = ((uint64_t)est_tile + 16u + 8u + 15u) & ~15ull;
+    return emf_tab_bytes(F->ns, F->K, F->r) + 16u * need <= EMF_LDS;
 }
 
 void fsm_free(FsmDev *fd) {
@@ -1567,7 +1624,7 @@ static int fsm_grids(FsmDev *fd) {
     if (pc < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
     fd->grid_c = (uint32_t)(pc * ncu);
     fd->grid_cm = 0;
-    const kcnt_t km = fd->cm > 1 ? kcntm_for(sw, fd->cb, fd->cm) : nullptr;
+    const kcntm_t km = fd->cm > 1 ? kcntm_for(sw, fd->cb, fd->cm) : nullptr;
     if (km) {
         int pm = 0;
         FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, km, 64 * cntm_cw(fd->cm), lds_cnt(fd)));
@@ -1677,13 +1734,17 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
         // TAIL launch
         const uint64_t nct = fd->grid_cm ? nc / fd->cm : 0;
         if (nct) {
+            // (the tiles after the count tiles: the launch's first workgroups)
             const uint32_t cwm = cntm_cw(fd->cm);
+            const uint64_t nu = nt - nct * fd->cm;
+            const uint32_t ntb = (uint32_t)((nu + cwm - 1) / cwm);
             const uint64_t nwg = (nct + cwm - 1) / cwm;
-            const uint32_t gc = (uint32_t)(nwg < fd->grid_cm ? nwg : fd->grid_cm);
+            const uint32_t gm = fd->grid_cm > ntb + 1 ? fd->grid_cm - ntb : 1u;
+            const uint32_t gc = (uint32_t)(nwg < gm ? nwg : gm) + ntb;
             hipLaunchKernelGGL(kcntm_for(sw, fd->cb, fd->cm), dim3(gc), dim3(64 * cwm), lds_cnt(fd), st, (const uint32_t *)d_data, geo,
-                               tab, wk, (uint64_t)0, nct);
+                               tab, wk, (uint64_t)0, nct, nct * fd->cm, nt, ntb);
             FS_OK(hipGetLastError());
-            nc = nct * fd->cm;
+            nc = nt;
         } else if (nc) {
             const uint64_t nwg = (nc + CW - 1) / CW;
             const uint32_t gc = (uint32_t)(nwg < fd->grid_c ? nwg : fd->grid_c);
@@ -1697,32 +1758,36 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
             FS_OK(hipGetLastError());
         }
     }
-    FS_OK(hipEventRecord(ev[1], st));
+    if (fd->phases) FS_OK(hipEventRecord(ev[1], st));
     hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk);
     FS_OK(hipGetLastError());
     hipLaunchKernelGGL(k_fscan2, dim3(1), dim3(1024), 0, st, geo, wk, nblk, ws->d_res + 16 * slot);
     FS_OK(hipGetLastError());
-    FS_OK(hipEventRecord(ev[2], st));
+    if (fd->phases) FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
         const uint32_t ew = emf_waves(emf_nch()), ew1 = emf_waves(1);
-        // tiles that end before the stream, then the last one(s) (TAIL)
+        // tiles that end before the stream, then the last one(s) (TAIL: the
+        // main launch's first workgroups; a launch of its own without tiles
+        // before them)
         const uint64_t ne = std::max<uint64_t>(emit_from, std::min<uint64_t>(bits / TB, nt));
+        const uint32_t ntb = (uint32_t)((nt - ne + ew1 - 1) / ew1);
         if (ne > emit_from) {
             const uint64_t nwg = (ne - emit_from + ew - 1) / ew;
-            const uint32_t ge = (uint32_t)(nwg < fd->grid_e ? nwg : fd->grid_e);
+            const uint32_t gm = fd->grid_e > ntb + 1 ? fd->grid_e - ntb : 1u;
+            const uint32_t ge = (uint32_t)(nwg < gm ? nwg : gm) + ntb;
             hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch(), fd->sco, fd->swz), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne,
-                               (uint32_t)lds_emf(fd));
+                               (uint32_t)lds_emf(fd), ne, nt, ntb);
             FS_OK(hipGetLastError());
-        }
-        if (ne < nt) {
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, true, 1, false), dim3((unsigned)((nt - ne + ew1 - 1) / ew1)), dim3(64 * ew1),
-                               lds_emf(fd), st, (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt,
-                               (uint32_t)lds_emf(fd));
+        } else if (ne < nt) {
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, true, 1, false), dim3(ntb), dim3(64 * ew1), lds_emf(fd), st,
+                               (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt,
+                               (uint32_t)lds_emf(fd), (uint64_t)0, (uint64_t)0, 0u);
             FS_OK(hipGetLastError());
         }
     }
     FS_OK(hipEventRecord(ev[3], st));
+    pd->phases = fd->phases;
     pd->nt = nt;
     pd->emit_from = emit_from;
     pd->cap = cap;
@@ -1742,9 +1807,16 @@ int fsm_collect(FsmWs *ws, hipEvent_t *ev, const FsmPend *pd, uint64_t *total, u
     *leave = res[4];
     *entry = res[5];
     if (emit_from >= nt) *total = 0;
-    (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
-    (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
-    (void)hipEventElapsedTime(&ms[2], ev[2], ev[3]);
+    if (pd->phases) {
+        (void)hipEventElapsedTime(&ms[0], ev[0], ev[1]);
+        (void)hipEventElapsedTime(&ms[1], ev[1], ev[2]);
+        (void)hipEventElapsedTime(&ms[2], ev[2], ev[3]);
+        ms[3] = ms[0] + ms[1] + ms[2];
+    } else {
+        // (no events between the kernels: each costs ~6 us of idle GPU)
+        ms[0] = ms[1] = ms[2] = 0.0f;
+        (void)hipEventElapsedTime(&ms[3], ev[0], ev[3]);
+    }
     if (fl & FF_FAIL) return HH_NOSYNC;
     if (*total > cap) return HH_ERR_CAPACITY;
     return HH_OK;

@@ -22,6 +22,7 @@ struct FsmDev {
     uint32_t grid_c, grid_e, sized_S, sized_ns, sized_K, sized_sco, sized_cb, sized_swz;
     uint32_t grid_cm;        // k_cntm's grid (0: no k_cntm for this tree / HH_CNT_M=1)
     uint32_t cm;             // regions per lane of the count pass (k_cntm, 2 or 4; 1: k_cnt only)
+    uint32_t phases;         // events between the count, scan and emission kernels (HH_FLAG_PHASE_TIMING)
     uint32_t sized_cm;
     uint32_t sco;            // k_emf's static copy-out (the default; HH_EMF_SCO=0: the store loop)
     uint32_t swz;            // k_emf's swizzled staging: codes whose lengths differ by at most 1 bit
@@ -31,8 +32,8 @@ struct FsmDev {
 // One decode of tiles [0, ntiles) of the segment at d_data (bits readable
 // stream bits), the first `emit_from` a prologue, tile 0 entered in state
 // in_state.  Outputs: *total symbols written to d_out, *leave (state after
-// the last tile), *entry (state entering tile emit_from).  ms[0..2]: count,
-// scan, emission device time.  Returns HH_OK, HH_ERR_CAPACITY, HH_ERR_DEVICE,
+// the last tile), *entry (state entering tile emit_from).  ms[0..3]: count,
+// scan, emission device time (fd->phases; else 0), the whole pipeline's.  Returns HH_OK, HH_ERR_CAPACITY, HH_ERR_DEVICE,
 // HH_ERR_NOMEM, HH_ERR_UNSUPPORTED (no tables) or the internal HH_NOSYNC
 // (chains that did not meet within HH_FSM_KM regions: a code that does not
 // resynchronise; never returned through the C ABI -- the callers take the
@@ -50,7 +51,7 @@ struct FsmWs {
 // What fsm_collect needs of a decode fsm_launch enqueued.
 struct FsmPend {
     uint64_t nt, emit_from, cap;
-    uint32_t slot;
+    uint32_t slot, phases;
 };
 void fsm_ws_free(FsmWs *ws);
 int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
@@ -65,7 +66,7 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
 int fsm_collect(FsmWs *ws, hipEvent_t *ev, const FsmPend *pd, uint64_t *total, uint32_t *leave, uint32_t *entry,
                 float *ms);
 int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, uint32_t maxlen);
-bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile);   // 7-bit steps leave room for 16 stagings
+bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile);   // F's emission tables leave room for 16 stagings
 void fsm_free(FsmDev *fd);
 int fsm_debug_arrays(const FsmWs *ws, uint64_t nt, uint32_t *rec, uint32_t *fx, int32_t *tsum, uint32_t *xs);
 

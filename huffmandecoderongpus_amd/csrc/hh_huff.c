@@ -471,7 +471,7 @@ int hh_fsm_build(const void *tv, uint32_t S, uint32_t Kreq, hh_fsm_tables *F) {
         }
     }
     if (ns == 0 || st[0] != 0) { rc = HH_ERR_UNSUPPORTED; goto out; }
-    if (Kreq != 0 && Kreq != 6 && Kreq != 7) { rc = HH_ERR_ARG; goto out; }
+    if (Kreq != 0 && (Kreq < 4 || Kreq > 7)) { rc = HH_ERR_ARG; goto out; }
     {
         /* the count step: a 16-bit entry holds the next row (state << (CB + 1)) */
         const uint32_t cb = ns <= HH_FSM_MAXS8 && S % 8 == 0 ? 8u : 7u;

@@ -141,6 +141,13 @@ typedef struct {
                                    k_walk, k_table, k_scan, k_emit) instead of
                                    the state-machine decode (k_cnt, k_fscan,
                                    k_emf) */
+#define HH_FLAG_PHASE_TIMING 16 /* record a HIP event between the count, scan
+                                   and emission kernels of every decode, for
+                                   ms_sync / ms_scan / ms_emit (each event
+                                   adds ~6 us of idle GPU time between the
+                                   kernels it separates; without the flag
+                                   only ms_total is measured, the phase times
+                                   read 0) */
 
 int hh_decoder_create(hh_decoder **dec, const hh_config *cfg);
 void hh_decoder_destroy(hh_decoder *dec);
@@ -152,10 +159,10 @@ int hh_decoder_set_tree(hh_decoder *dec, const hh_tree *tree);
 /* Statistics of the last decode (device time of each phase, in ms). */
 typedef struct {
     double ms_total;         /* hipEvent time of the whole device pipeline  */
-    double ms_sync;          /* front kernel: speculative region decode,
-                                walks, tile transfer tables                 */
-    double ms_scan;          /* scan kernels: tile entering states, offsets */
-    double ms_emit;          /* emit kernel: exact runs decoded to HBM      */
+    double ms_sync;          /* count kernels: heads, region counts, walks
+                                (state machine: HH_FLAG_PHASE_TIMING only)  */
+    double ms_scan;          /* scan kernels: tile bases, total (idem)      */
+    double ms_emit;          /* emission kernels: symbols to HBM (idem)     */
     uint64_t out_len;        /* symbols decoded                              */
     uint64_t lanes;          /* lane regions                                 */
     uint64_t repairs;        /* 1: a tile-state chain was composed on the

@@ -39,7 +39,18 @@ per_kernel = {}
 for i in keep:
     for s, e, k, _ in decodes[i]:
         per_kernel.setdefault(k, []).append((e - s) * 1e-6)
+# the idle time inside a decode: each gap between one kernel's end and the
+# next one's start (launch order), and the gap before the next decode
+gaps = {}
+for i in keep:
+    d = decodes[i]
+    for a in range(1, len(d)):
+        gaps.setdefault(a, []).append((d[a][0] - d[a - 1][1]) * 1e-3)
+between = [(decodes[i + 1][0][0] - decodes[i][-1][1]) * 1e-3 for i in keep if i + 1 < len(decodes)]
 res = {"decodes": len(keep),
+       "launches_per_decode": round(statistics.mean(len(decodes[i]) for i in keep), 2),
+       "gap_us_after_launch": {a: round(statistics.mean(v), 2) for a, v in gaps.items()},
+       "gap_us_between_decodes": round(statistics.mean(between), 2) if between else None,
        "ms_kernel_sum": round(statistics.mean(sums[i] for i in keep), 4),
        "ms_span": round(statistics.mean(spans[i] for i in keep), 4),
        "per_decode_ms": {k: round(sum(v) / len(keep), 4) for k, v in per_kernel.items()}}

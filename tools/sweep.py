@@ -51,9 +51,6 @@ for mib in sizes:
     C, D = syn.compressed_bytes, syn.decoded_bytes
     row = {"MiB": mib, "bits": syn.bits, "decoded_bytes": D, "ok": bool(ok),
            "ms_total": round(t, 4),
-           "ms_front": round(statistics.median(s["ms_sync"] for s in ms), 4),
-           "ms_scan": round(statistics.median(s["ms_scan"] for s in ms), 4),
-           "ms_emit": round(statistics.median(s["ms_emit"] for s in ms), 4),
            "decoded_MBps": round(D / (t * 1e-3) / 1e6, 1),
            "ms_step_async": round(ms_step, 4), "decoded_MBps_wall": round(D / (ms_step * 1e-3) / 1e6, 1),
            "roofline_frac": round((C + D) / (t * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

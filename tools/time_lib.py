@@ -46,7 +46,9 @@ def verify(out, n):
     if hf is None:
         return n == syn.decoded_bytes and bool(torch.equal(out[:n], syn.syms))
     return n == syn.decoded_bytes and synth.verify_tiled(out, syn)
-dec = H.Decoder(0, lane_bits=int(os.environ.get("HH_LANE_BITS", "0")), flags=int(os.environ.get("HH_FLAGS", "0")))
+# (with the phase events between the kernels: the A/B tables report the split)
+dec = H.Decoder(0, lane_bits=int(os.environ.get("HH_LANE_BITS", "0")),
+                flags=int(os.environ.get("HH_FLAGS", "0")) | (0 if os.environ.get("HH_NO_PHASES") else H.FLAG_PHASE_TIMING))
 dec.set_tree(syn.tree)
 out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device="cuda")
 ph = {"total": [], "sync": [], "scan": [], "emit": []}
