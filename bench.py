@@ -421,7 +421,7 @@ def main():
     phases = (phase_split(local, syn.tree, 0, syn.data, syn.bits, out) if world == 1
               else {"sync": None, "scan": None, "emit": None})
     fast = all(s["exact_fallback"] == 0 for s in dev_ms)
-    kernels = ("k_cnt+k_fscan1+k_fscan2+k_emf" if all(s["state_machine"] for s in dev_ms)
+    kernels = ("k_cntm+k_fscan1+k_fscan2+k_emf" if all(s["state_machine"] for s in dev_ms)
                else "k_front+k_walk+k_table+k_scan1+k_scan2+k_emit")
     extra = {}
     if world > 1:

@@ -12,7 +12,7 @@ import os
 import statistics
 import sys
 
-NAMES = ("k_cnt", "k_fscan1", "k_fscan2", "k_emf", "k_fixed")
+NAMES = ("k_cntm", "k_cnt", "k_fscan1", "k_fscan2", "k_emf", "k_fixed")
 rows = []
 for path in glob.glob(os.path.join(sys.argv[1], "**", "*kernel_trace.csv"), recursive=True):
     with open(path) as f:
@@ -25,7 +25,7 @@ rows.sort()
 # a decode starts at each k_cnt whose predecessor was a k_emf (or the first)
 decodes, cur = [], []
 for r in rows:
-    if r[2] == "k_cnt" and cur and cur[-1][2] == "k_emf":
+    if r[2] in ("k_cnt", "k_cntm") and cur and cur[-1][2] == "k_emf":
         decodes.append(cur)
         cur = []
     cur.append(r)

@@ -21,7 +21,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_front", "k_walk", "k_table", "k_scan1", "k_scan2", "k_emitx", "k_emit", "k_cnt", "k_fscan1", "k_fscan2", "k_emf")   # (k_emitx before k_emit: names match by substring)
+KERNELS = ("k_front", "k_walk", "k_table", "k_scan1", "k_scan2", "k_emitx", "k_emit", "k_cntm", "k_cnt", "k_fscan1", "k_fscan2", "k_emf")   # (k_emitx before k_emit: names match by substring)
 
 
 def kname(s):
