@@ -175,6 +175,7 @@ def phase_split(device: int, tree, flags: int, data, bits: int, out, n: int = 3)
     HH_FLAG_PHASE_TIMING (events between the kernels, ~6 us of idle GPU
     each: never in the timed decodes), after the timed region."""
     import torch
+    import huffmandecoderongpus_amd as H
     d = H.Decoder(device, flags=flags | H.FLAG_PHASE_TIMING)
     try:
         d.set_tree(tree)
