@@ -755,8 +755,21 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
 // cntm_waves(M) waves per SIMD (a lane holds its whole span of M regions:
 // more than k_cnt's 64 VGPRs).  M = 2: 24 waves per CU in 3 workgroups of 8
 // (80 VGPRs); M = 4: 20 in 2 of 10 (96 VGPRs); each workgroup its tables.
-__host__ __device__ constexpr uint32_t cntm_cw(uint32_t m) { return m >= 4 ? 10u : 8u; }
-__host__ __device__ constexpr uint32_t cntm_waves(uint32_t m) { return m >= 4 ? 5u : 6u; }
+#ifndef HH_CNTM2_CW
+#define HH_CNTM2_CW 8
+#endif
+#ifndef HH_CNTM2_WAVES
+#define HH_CNTM2_WAVES 6
+#endif
+#ifndef HH_CNTM7_CW
+#define HH_CNTM7_CW 12
+#endif
+// (cb 7: 65 KB count tables for 255 states -- two workgroups per CU, of 12
+// waves: byte alphabet count 0.51 -> 0.43 ms against 8)
+__host__ __device__ constexpr uint32_t cntm_cw(uint32_t m, uint32_t cb = 8) {
+    return m >= 4 ? 10u : cb == 7 ? HH_CNTM7_CW : HH_CNTM2_CW;
+}
+__host__ __device__ constexpr uint32_t cntm_waves(uint32_t m) { return m >= 4 ? 5u : HH_CNTM2_WAVES; }
 #ifndef HH_CNT_M
 #define HH_CNT_M 2            // regions per lane of the count pass: 2, 4 (k_cntm) or 1 (k_cnt; HH_CNT_M=n overrides)
 #endif
@@ -806,10 +819,10 @@ __device__ __noinline__ CntmWalk cntm_walk(const uint32_t *b1, const uint32_t *_
 }
 
 template <uint32_t SW, uint32_t CB, uint32_t M>
-__global__ __launch_bounds__(64 * cntm_cw(M)) __attribute__((amdgpu_waves_per_eu(cntm_waves(M), 8))) void k_cntm(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+__global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_per_eu(cntm_waves(M), 8))) void k_cntm(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                   uint64_t c0, uint64_t c1, uint64_t u0, uint64_t u1, uint32_t ntb) {
     static_assert((32 * SW) % CB == 0 && 64 % M == 0, "whole count steps per region, lanes in whole emission tiles");
-    constexpr uint32_t CWM = cntm_cw(M);
+    constexpr uint32_t CWM = cntm_cw(M, CB);
     // the first ntb workgroups (dispatched first, resident beside the rest):
     // the emission tiles [u0, u1) after the count tiles, one per wave with
     // the stream-end checks (TAIL) -- a launch of their own after this one
@@ -1627,7 +1640,7 @@ static int fsm_grids(FsmDev *fd) {
     const kcntm_t km = fd->cm > 1 ? kcntm_for(sw, fd->cb, fd->cm) : nullptr;
     if (km) {
         int pm = 0;
-        FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, km, 64 * cntm_cw(fd->cm), lds_cnt(fd)));
+        FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, km, 64 * cntm_cw(fd->cm, fd->cb), lds_cnt(fd)));
         fd->grid_cm = pm > 0 ? (uint32_t)(pm * ncu) : 0u;
     }
     fd->grid_e = (uint32_t)(pe * ncu);
@@ -1735,7 +1748,7 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
         const uint64_t nct = fd->grid_cm ? nc / fd->cm : 0;
         if (nct) {
             // (the tiles after the count tiles: the launch's first workgroups)
-            const uint32_t cwm = cntm_cw(fd->cm);
+            const uint32_t cwm = cntm_cw(fd->cm, fd->cb);
             const uint64_t nu = nt - nct * fd->cm;
             const uint32_t ntb = (uint32_t)((nu + cwm - 1) / cwm);
             const uint64_t nwg = (nct + cwm - 1) / cwm;
