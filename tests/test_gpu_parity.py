@@ -397,11 +397,43 @@ def test_emission_staging_variants(hh, files_dir, env, monkeypatch):
         dec.close()
 
 
-@pytest.mark.parametrize("m", ["2", "4"])
+def test_phase_timing_flag(hh, files_dir):
+    """HH_FLAG_PHASE_TIMING: events between the count, scan and emission
+    kernels give the per-kernel split (ms_sync / ms_scan / ms_emit, summing
+    to ms_total); without it only ms_total is measured (the split reads 0).
+    The bytes are the same either way."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    hf, text = synth.load_source(files_dir, "kjv.txt")
+    syn = synth.tiled_stream(hf, text, 16 << 20)
+    outs = []
+    for flags in (0, hh.FLAG_PHASE_TIMING):
+        dec = hh.Decoder(0, flags=flags)
+        try:
+            dec.set_tree(syn.tree)
+            out = torch.zeros(syn.decoded_bytes + 64, dtype=torch.uint8, device="cuda")
+            n = dec.decode_device(syn.data, syn.bits, out)
+            torch.cuda.synchronize()
+            st = dec.stats()
+            assert n == syn.decoded_bytes and st["state_machine"] == 1
+            assert st["ms_total"] > 0
+            split = (st["ms_sync"], st["ms_scan"], st["ms_emit"])
+            if flags:
+                assert all(x > 0 for x in split), st
+                assert abs(sum(split) - st["ms_total"]) < 1e-3 * max(1.0, st["ms_total"]), st
+            else:
+                assert split == (0.0, 0.0, 0.0), st
+            outs.append(out)
+        finally:
+            dec.close()
+    assert torch.equal(outs[0], outs[1]) and synth.verify_tiled(outs[0], syn)
+
+
+@pytest.mark.parametrize("m", ["1", "2", "4"])
 def test_count_pass_regions_per_lane(hh, files_dir, m, monkeypatch):
     """The count pass with m consecutive regions per lane (k_cntm: one head
-    per lane, the walks read back and rewrite the successor lane's records)
-    gives the same bytes as the oracle: the kjv- and E.coli-tiled streams
+    per lane, the walks read back and rewrite the successor lane's records;
+    m = 1: k_cnt, a region per lane) gives the same bytes as the oracle: the kjv- and E.coli-tiled streams
     (the latter through the state machine), cut streams of a 40-leaf and of
     a 256-leaf random tree (7-bit count steps) whose lengths leave partial
     count tiles to the tail launch, and segments entered after a prologue."""
