@@ -96,6 +96,8 @@ _SIGS = {
     "hh_encode_bound": ([C.POINTER(_Tree), C.c_uint64], C.c_uint64),
     "hh_encode": ([C.POINTER(_Tree), C.c_void_p, C.c_uint64, C.c_void_p,
                    C.POINTER(C.c_uint64)], C.c_int),
+    "hh_encode_device": ([C.POINTER(_Tree), C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                          C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
     "hh_decoder_create": ([C.POINTER(C.c_void_p), C.POINTER(_Config)], C.c_int),
     "hh_decoder_destroy": ([C.c_void_p], None),
     "hh_decoder_set_tree": ([C.c_void_p, C.POINTER(_Tree)], C.c_int),
@@ -234,6 +236,19 @@ class Tree:
                                C.byref(bits)), "encode")
         nb = (bits.value + 7) // 8
         return out[: nb + PAYLOAD_PAD].copy(), int(bits.value)
+
+
+def encode_device(tree: "Tree", syms, out, stream=None) -> int:
+    """Pack torch uint8 CUDA symbols with tree's codes into the torch uint8
+    CUDA tensor out (hh_encode_device; out must hold the stream rounded up
+    to 32-bit words, plus PAYLOAD_PAD for a decode).  Returns the bits."""
+    import torch
+    assert syms.is_cuda and out.is_cuda and syms.dtype == torch.uint8 and out.dtype == torch.uint8
+    bits = C.c_uint64(0)
+    _check(lib().hh_encode_device(C.byref(tree._c), syms.data_ptr(), syms.numel(), out.data_ptr(), out.numel(),
+                                  C.byref(bits), stream.cuda_stream if stream is not None else None),
+           "encode_device")
+    return int(bits.value)
 
 
 class Decoder:

@@ -834,7 +834,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS, LG = 64 / M;   // LG: lanes per emission tile
     constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
-    constexpr uint32_t HWL = HeadGeo<SW, CB>::HWL;
     const uint32_t ns = geo.ns, tid = threadIdx.x, j = tid & 63u;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     uint32_t *s_b1 = (uint32_t *)(smem + (ns << (CB + 1)));

@@ -226,6 +226,20 @@ static int build_codebook(const hh_tree *t, codebook *cb) {
     return HH_OK;
 }
 
+/* The code table for the device encoder (csrc/hh_encode.hip): len 0 for a
+ * symbol absent from the tree. */
+int hh_codebook(const void *tv, uint64_t code[256], uint8_t len[256]) {
+    codebook cb;
+    int rc = build_codebook((const hh_tree *)tv, &cb);
+    if (rc) return rc;
+    for (int i = 0; i < 256; i++) {
+        if (cb.have[i] && cb.len[i] == 0) return HH_ERR_UNSUPPORTED;   /* (a one-leaf tree: codes of no bits) */
+        code[i] = cb.code[i];
+        len[i] = cb.have[i] ? cb.len[i] : 0;
+    }
+    return HH_OK;
+}
+
 uint64_t hh_encode_bound(const hh_tree *t, uint64_t n) {
     hh_tree_info in;
     if (hh_tree_check(t, &in)) return 0;

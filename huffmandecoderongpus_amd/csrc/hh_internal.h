@@ -107,6 +107,8 @@ extern "C" {
 #endif
 /* Builds the tables; returns HH_OK or an hh_status. */
 int hh_tables_build(const void *tree /* const hh_tree* */, hh_tables *t);
+/* The encoder's code table (first stream bit in bit 0; len 0: absent). */
+int hh_codebook(const void *tree /* const hh_tree* */, uint64_t code[256], uint8_t len[256]);
 #ifdef __cplusplus
 }
 #endif

@@ -113,6 +113,13 @@ hh_tree hh_huff_tree(const hh_huff *h);
 uint64_t hh_encode_bound(const hh_tree *tree, uint64_t n);
 int hh_encode(const hh_tree *tree, const uint8_t *syms, uint64_t n,
               uint8_t *out, uint64_t *bits);
+/* The same on the GPU: n symbols at device pointer d_syms packed into
+ * device buffer d_out (cap bytes, 4-byte aligned; it must hold the stream
+ * rounded up to whole 32-bit words -- hh_encode_bound always does).  The
+ * same bytes as hh_encode.  *bits gets the length (also with
+ * HH_ERR_CAPACITY).  Enqueued on hip_stream; returns when done. */
+int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_t n,
+                     void *d_out, uint64_t cap, uint64_t *bits, void *hip_stream);
 
 /* ---------------------------------------------------------------------- */
 /* Device decoder.                                                        */

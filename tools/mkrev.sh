@@ -12,6 +12,7 @@ F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-unused-result -Wno-unused-val
 /opt/rocm/bin/hipcc $F -c $D/csrc/hh_fsm.hip -o $D/hh_fsm.o &
 gcc -O3 -fPIC -std=gnu11 -I$D/include -I$D/csrc -c $D/csrc/hh_huff.c -o $D/hh_huff.o &
 gcc -O3 -fPIC -std=gnu11 -I$D/include -I$D/csrc -c $D/csrc/hh_plugin.c -o $D/hh_plugin.o &
+[ -f $D/csrc/hh_encode.hip ] && /opt/rocm/bin/hipcc $F -c $D/csrc/hh_encode.hip -o $D/hh_encode.o &
 wait
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o build/var/$N.so $D/*.o
 rm -rf $D
