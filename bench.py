@@ -256,6 +256,42 @@ def evaluate_scope(H, hf, payload, bits: int, n_want: int, reps: int, check=None
         dec.close()
 
 
+def encode_rate(H, hf, text, n: int, dev, reps: int = 5) -> dict:
+    """The device encoder (hh_encode_device) on the headline's symbols (the
+    kjv text tiled to n bytes, resident in HBM) with kjv.txt.huff's codes:
+    wall time per call (it synchronises), the stream checked against the
+    decoder's input bits.  HBM-bound: 1 B read per symbol, its bits
+    written, plus the output's zeroing."""
+    import numpy as np
+    import torch
+    tree = hf.tree()
+    t = torch.from_numpy(np.ascontiguousarray(text)).to(dev)
+    syms = t.repeat(n // t.numel() + 1)[:n]
+    del t
+    out = torch.empty((n * 24 + 31) // 32 * 4 + 64, dtype=torch.uint8, device=dev)
+    bits = H.encode_device(tree, syms, out)
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        H.encode_device(tree, syms, out)
+        ts.append(time.perf_counter() - t0)
+    ms = statistics.median(ts) * 1e3
+    dec = H.Decoder(dev.index or 0)
+    try:
+        dec.set_tree(tree)
+        back = torch.empty(n + 4096, dtype=torch.uint8, device=dev)
+        ok = dec.decode_device(out, bits, back) == n and bool(torch.equal(back[:n], syms))
+        del back
+    finally:
+        dec.close()
+    del out, syms
+    torch.cuda.empty_cache()
+    return {"ok": ok, "symbols": n, "bits": bits, "ms": round(ms, 3),
+            "symbols_MBps": round(n / (ms * 1e-3) / 1e6, 1),
+            "hbm_GBps": round((n + 2 * (bits + 7) // 8) / (ms * 1e-3) / 1e9, 1)}
+
+
 def copy_rate(dev, nbytes: int, reps: int = 5) -> dict:
     """Device-to-device copy of `nbytes` on the same GPU (torch copy_,
     read + write = 2 x nbytes moved): the HBM rate a streaming kernel
@@ -531,6 +567,7 @@ def main():
             lambda o: synth.verify_tiled(torch.from_numpy(o).to(dev), syn))
         del host_pay
         res["evaluate"] = ev
+        res["encode"] = encode_rate(H, hf, text, syn.decoded_bytes, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(a.files, a.cpu_seconds)
         from oracle import oracle as O

@@ -45,6 +45,20 @@ __device__ __forceinline__ uint32_t enc_block_sum(uint32_t v, uint32_t *s_w) {
     return t;
 }
 
+// A thread's ENC_PT symbols from i0: one 16-B load when they are all in the
+// stream and 16-B aligned (torch tensors are), else byte by byte.
+__device__ __forceinline__ void enc_load16(const uint8_t *__restrict__ syms, uint64_t n, uint64_t i0, uint8_t *sy) {
+    if (i0 + ENC_PT <= n && (((uintptr_t)(syms + i0)) & 15u) == 0) {
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        const u4 v = __builtin_nontemporal_load((const u4 *)(syms + i0));
+#pragma unroll
+        for (uint32_t k = 0; k < ENC_PT; k++) sy[k] = (uint8_t)(v[k >> 2] >> (8 * (k & 3)));
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < ENC_PT; k++) sy[k] = i0 + k < n ? syms[i0 + k] : 0u;
+    }
+}
+
 __global__ __launch_bounds__(ENC_TB) void k_enc_len(const uint8_t *__restrict__ syms, uint64_t n,
                                                     const EncTab *__restrict__ tab, uint64_t *__restrict__ cbits,
                                                     uint32_t *__restrict__ bad) {
@@ -54,12 +68,14 @@ __global__ __launch_bounds__(ENC_TB) void k_enc_len(const uint8_t *__restrict__ 
     s_len[tid] = tab->len[tid];
     __syncthreads();
     const uint64_t i0 = (uint64_t)blockIdx.x * ENC_CH + (uint64_t)tid * ENC_PT;
+    uint8_t sy[ENC_PT];
+    enc_load16(syms, n, i0, sy);
     uint32_t sum = 0;
     bool miss = false;
 #pragma unroll
     for (uint32_t k = 0; k < ENC_PT; k++)
         if (i0 + k < n) {
-            const uint32_t l = s_len[syms[i0 + k]];
+            const uint32_t l = s_len[sy[k]];
             sum += l;
             miss |= l == 0;
         }
@@ -122,12 +138,10 @@ __global__ __launch_bounds__(ENC_TB) void k_enc_pack(const uint8_t *__restrict__
     // this thread's symbols and their bits
     const uint64_t i0 = (uint64_t)blockIdx.x * ENC_CH + (uint64_t)tid * ENC_PT;
     uint8_t sy[ENC_PT];
+    enc_load16(syms, n, i0, sy);
     uint32_t sum = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < ENC_PT; k++) {
-        sy[k] = i0 + k < n ? syms[i0 + k] : 0u;
-        sum += i0 + k < n ? s_len[sy[k]] : 0u;
-    }
+    for (uint32_t k = 0; k < ENC_PT; k++) sum += i0 + k < n ? s_len[sy[k]] : 0u;
     // exclusive scan of the threads' bits within the chunk
     uint32_t x = sum;
 #pragma unroll
