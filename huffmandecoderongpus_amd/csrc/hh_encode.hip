@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "hiphuff.h"
 #include "hh_internal.h"
 
@@ -192,10 +194,27 @@ extern "C" int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_
     const uint64_t nch = (n + ENC_CH - 1) / ENC_CH;
     if (nch > 0x7fffffffull) return HH_ERR_UNSUPPORTED;
     // workspace: the table, the chunks' bits / offsets, the total and the
-    // absent-symbol flag
-    uint8_t *ws = nullptr;
+    // absent-symbol flag -- kept across calls per device (grown when a call
+    // needs more; one call at a time per process: a per-call allocation and
+    // free cost more than the kernels at 64 MiB)
     const size_t o_cb = (sizeof(EncTab) + 255) & ~(size_t)255, o_res = o_cb + ((nch * 8 + 255) & ~(size_t)255);
-    if (hipMalloc(&ws, o_res + 64) != hipSuccess) return HH_ERR_NOMEM;
+    static std::mutex mu;
+    static uint8_t *s_ws[64];
+    static size_t s_sz[64];
+    std::lock_guard<std::mutex> lock(mu);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return HH_ERR_DEVICE;
+    if (s_sz[dev] < o_res + 64) {
+        if (s_ws[dev]) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(s_ws[dev]);
+            s_ws[dev] = nullptr;
+            s_sz[dev] = 0;
+        }
+        if (hipMalloc(&s_ws[dev], o_res + 64) != hipSuccess) return HH_ERR_NOMEM;
+        s_sz[dev] = o_res + 64;
+    }
+    uint8_t *ws = s_ws[dev];
     EncTab *d_tab = (EncTab *)ws;
     uint64_t *d_cb = (uint64_t *)(ws + o_cb), *d_res = (uint64_t *)(ws + o_res);
     uint32_t *d_bad = (uint32_t *)(ws + o_res + 32);
@@ -223,6 +242,5 @@ extern "C" int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_
         if (hipStreamSynchronize(st) != hipSuccess) break;
         rc = HH_OK;
     } while (0);
-    (void)hipFree(ws);
     return rc;
 }
