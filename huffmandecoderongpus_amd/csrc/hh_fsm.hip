@@ -1115,6 +1115,9 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
 // when it is full (the last, partial one after the last step).  The unused
 // bytes of every stored dword are zero: a dword shared with the
 // neighbouring runs is repaired by OR afterwards (emf_edges).
+#ifndef HH_EMF_CPOL
+#define HH_EMF_CPOL 2         // k_emf's static copy-out stores: cache policy bits (2: nt -- 1 GiB kjv -3 % against plain)
+#endif
 #ifndef HH_EMF_STFULL
 #define HH_EMF_STFULL 1       // k_emf: a step stores its dword only when full (0: every step)
 #endif
@@ -1447,7 +1450,7 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
                             const uint32_t lo = 16 * (j + 64 * ii);
                             u32x4 v = {0u, 0u, 0u, 0u};
                             if (lo < end) v = emf_read16<SWZ>(smem, (uint32_t)(sb - smem) + lo);   // (LDS reads only where the tile has bytes)
-                            __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(lo >= a0[x] ? lo : 0x40000000u), 0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(lo >= a0[x] ? lo : 0x40000000u), 0, HH_EMF_CPOL);
                         }
                         __builtin_amdgcn_raw_buffer_store_b8(smem[emf_swz<SWZ>((uint32_t)(sb - smem) + q)], ors, (int)(pb ? q : 0x40000000u), 0, 0);
                     } else {
