@@ -190,12 +190,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t fs_rsrc(const uint32_t *g, uin
     return __builtin_amdgcn_make_buffer_rsrc((void *)(g + w0), 0, (int)nbytes, 0x00020000);
 }
 // SW words from word offset wo of the resource
+#ifndef HH_LD_CPOL
+#define HH_LD_CPOL 0          // payload loads' cache policy bits (2: nt)
+#endif
 template <uint32_t SW>
 __device__ __forceinline__ void fs_load(uint32_t *v, __amdgpu_buffer_rsrc_t rs, uint32_t wo) {
     if (SW % 4 == 0) {
 #pragma unroll
         for (uint32_t k = 0; k < SW; k += 4) {
-            const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, 0));
+            const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, HH_LD_CPOL));
             v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
         }
     } else {
@@ -861,7 +864,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
 #pragma unroll
             for (uint32_t k = 0; k < SW; k += 4)
                 if (k >= a && k < b) {
-                    const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, 0));
+                    const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, HH_LD_CPOL));
                     v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
                 }
         } else {
