@@ -47,7 +47,10 @@ $(BUILD)/hh_fsm.o: $(CSRC)/hh_fsm.hip $(CSRC)/hh_fsm_dev.h $(CSRC)/hh_fsm.h $(CS
 $(BUILD)/hh_encode.o: $(CSRC)/hh_encode.hip $(CSRC)/hh_internal.h include/hiphuff.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/hh_device.o $(BUILD)/hh_fsm.o $(BUILD)/hh_encode.o $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
+$(BUILD)/hh_probe.o: $(CSRC)/hh_probe.hip include/hiphuff.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(BUILD)/hh_device.o $(BUILD)/hh_fsm.o $(BUILD)/hh_encode.o $(BUILD)/hh_probe.o $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 
 $(CLI): $(PKG)/host/hh_cli.c $(LIB) include/hiphuff.h include/hiphuff_plugin.h
@@ -74,7 +77,7 @@ clean:
 
 # A/B variant of the library: make variant V=name HIPEXTRA="-DHH_X=1"
 # -> build/libhiphuff_<name>.so (tools/ab.sh)
-variant: $(BUILD)/hh_plugin.o $(BUILD)/hh_encode.o
+variant: $(BUILD)/hh_plugin.o $(BUILD)/hh_encode.o $(BUILD)/hh_probe.o
 	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/hh_device.hip -o $(BUILD)/hh_device_$(V).o
 	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/hh_fsm.hip -o $(BUILD)/hh_fsm_$(V).o
 	$(CC) $(CFLAGS) $(HIPEXTRA) -c $(CSRC)/hh_huff.c -o $(BUILD)/hh_huff_$(V).o

@@ -82,6 +82,7 @@ FLAG_FORCE_SEGMENT = 2
 FLAG_NO_FIXED = 4     # HH_FLAG_NO_FIXED: fixed-length codes through the general pipeline too
 FLAG_LEGACY = 8       # HH_FLAG_LEGACY: round 2's pipeline instead of the state-machine decode
 FLAG_PHASE_TIMING = 16  # HH_FLAG_PHASE_TIMING: events between the kernels (ms_sync/scan/emit)
+FLAG_KEEP_HOST_PINNED = 32  # HH_FLAG_KEEP_HOST_PINNED: decode_host keeps the caller's buffers page-locked
 _lib_handle: Optional[C.CDLL] = None
 
 # exported symbols and their ctypes signatures; tests check every one of these
@@ -110,8 +111,13 @@ _SIGS = {
     "hh_decoder_tile_bits": ([C.c_void_p, C.POINTER(C.c_uint64)], C.c_int),
     "hh_decode_device_range": ([C.c_void_p, C.c_void_p, C.POINTER(_Range), C.c_void_p,
                                 C.c_uint64, C.POINTER(_RangeOut), C.c_void_p], C.c_int),
+    "hh_decode_device_range_async": ([C.c_void_p, C.c_void_p, C.POINTER(_Range), C.c_void_p,
+                                      C.c_uint64, C.POINTER(_RangeOut), C.c_void_p], C.c_int),
+    "hh_decoder_release_host": ([C.c_void_p], C.c_int),
     "hh_decode_host": ([C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                         C.POINTER(C.c_uint64)], C.c_int),
+    "hh_copy_device": ([C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
+                        C.POINTER(C.c_float)], C.c_int),
     "hh_stage_initbitsindex": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p], C.c_int),
     "hh_stage_decodeallbits": ([C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                 C.c_void_p], C.c_int),
@@ -251,6 +257,31 @@ def encode_device(tree: "Tree", syms, out, stream=None) -> int:
     return int(bits.value)
 
 
+def copy_device(src, dst, nt: bool = False, stream=None) -> float:
+    """hh_copy_device on torch uint8 CUDA tensors (the same number of bytes,
+    a multiple of 16): the streaming-copy reference; returns its device ms."""
+    import torch
+    assert src.is_cuda and dst.is_cuda and src.numel() == dst.numel()
+    ms = C.c_float(0.0)
+    s = stream if stream is not None else torch.cuda.current_stream(src.device)
+    _check(lib().hh_copy_device(src.data_ptr(), dst.data_ptr(), src.numel(), int(nt), s.cuda_stream,
+                                C.byref(ms)), "copy_device")
+    return float(ms.value)
+
+
+class RangeResult:
+    """The hh_range_out of an asynchronous segment decode (valid once checked)."""
+
+    def __init__(self):
+        self._ro = _RangeOut()
+
+    def as_dict(self) -> dict:
+        ro = self._ro
+        return {"out_len": int(ro.out_len), "leave_state": int(ro.leave_state),
+                "const_seen": bool(ro.const_seen), "entry_state": int(ro.entry_state),
+                "entry_exact": bool(ro.entry_exact)}
+
+
 class Decoder:
     """Device decoder: tables + workspace on one GPU (hh_decoder_*)."""
 
@@ -296,6 +327,10 @@ class Decoder:
         _check(lib().hh_decode_host(self._h, payload.ctypes.data, bits, out.ctypes.data, cap,
                                     C.byref(n)), "decode_host")
         return out[: n.value]
+
+    def release_host(self) -> None:
+        """hh_decoder_release_host: unpin the buffers FLAG_KEEP_HOST_PINNED kept."""
+        _check(lib().hh_decoder_release_host(self._h), "release_host")
 
     def decode_device_ptr(self, d_data: int, bits: int, d_out: int, cap: int,
                           stream: int = 0) -> int:
@@ -353,6 +388,18 @@ class Decoder:
         return {"out_len": int(ro.out_len), "leave_state": int(ro.leave_state),
                 "const_seen": bool(ro.const_seen), "entry_state": int(ro.entry_state),
                 "entry_exact": bool(ro.entry_exact)}
+
+    def decode_range_async_ptr(self, d_data: int, bits_avail: int, ntiles: int, in_state: int,
+                               d_out: int, cap: int, stream: int = 0, prologue: int = 0) -> "RangeResult":
+        """hh_decode_device_range_async: enqueues the segment's decode and
+        returns a RangeResult whose fields are valid once the decode has been
+        checked (by the next asynchronous decode on this decoder, or wait())."""
+        rg = _Range(bits_avail, ntiles, prologue, in_state)
+        r = RangeResult()
+        self._pending.append(r)
+        _check(lib().hh_decode_device_range_async(self._h, d_data, C.byref(rg), d_out, cap,
+                                                  C.byref(r._ro), stream or None), "decode_range_async")
+        return r
 
     def stage_pipeline_ptr(self, d_data: int, bits: int, d_out: int, cap: int,
                            stream: int = 0) -> int:

@@ -1424,6 +1424,9 @@ struct hh_decoder {
     hipStream_t h2d, d2h;
     hipEvent_t *pipe_ev;
     uint32_t npipe_ev;
+    // caller buffers kept page-locked across calls (HH_FLAG_KEEP_HOST_PINNED)
+    const void *pin_p[2];
+    size_t pin_n[2];
     // the asynchronous decode not checked yet (hh_decode_device_async)
     struct {
         int active;
@@ -1434,6 +1437,7 @@ struct hh_decoder {
         void *d_out;
         uint64_t *out_len;
         hipStream_t st;
+        hh_range_out *ro;      // a segment's decode (hh_decode_device_range_async): its results
     } apend;
     int async_rc;              // the first failure since the last hh_decode_wait
     uint32_t async_seq;        // asynchronous decodes launched (the result slot alternates)
@@ -1496,6 +1500,7 @@ extern "C" void hh_decoder_destroy(hh_decoder *d) {
     if (!d) return;
     hipSetDevice(d->device);
     async_check(d);                     // (an asynchronous decode still running)
+    hh_decoder_release_host(d);
     if (d->ws) hipFree(d->ws);
     if (d->d_l1) hipFree(d->d_l1);
     if (d->d_l2) hipFree(d->d_l2);
@@ -2136,7 +2141,13 @@ static int async_check(hh_decoder *d) {
         rc = fsm_collect(&d->fsm_ws, ev, &d->apend.pd, &total, &leave, &en, ms);
         fsm_stats(d, d->apend.bits, total, ms);
         *d->apend.out_len = total;
-        if (rc == HH_NOSYNC) {
+        if (d->apend.ro) {
+            // a segment: its states; one that does not resynchronise is
+            // unsupported (decode such a code whole), as the synchronous call
+            d->apend.ro->leave_state = leave;
+            d->apend.ro->entry_state = en;
+            if (rc == HH_NOSYNC) rc = HH_ERR_UNSUPPORTED;
+        } else if (rc == HH_NOSYNC) {
             d->stats.repairs = 1;
             const bool seg_ok = d->ht->maxlen <= HH_MAXLEN_FAST && !(d->cfg.flags & HH_FLAG_FORCE_EXACT);
             d->stats.exact_fallback = seg_ok ? 2 : 1;
@@ -2177,6 +2188,13 @@ extern "C" int hh_decode_device_async(hh_decoder *d, const void *d_data, uint64_
         rc = fixed_path(d, d_data, bits, (uint8_t *)d_out, cap, &n, st, slot_ev(d, slot), false);
         *out_len = n;
     } else {
+        // The state-machine workspace (records, tile sums, corrections) is
+        // one per decoder: a decode queued on another stream than the
+        // pending one waits for that one's last kernel before its count pass
+        // may overwrite what the pending emission still reads.  (On one
+        // stream the order is the stream's.)
+        if (d->apend.active && !d->apend.fixed && d->apend.st != st)
+            HIP_OK(hipStreamWaitEvent(st, slot_ev(d, d->apend.pd.slot)[3], 0));
         rc = fsm_launch(&d->fsm, &d->fsm_ws, slot, slot_ev(d, slot), d_data, bits, 0, 0, 0, d_out, cap, st, &pd);
     }
     async_check(d);                     // the previous decode, while this one runs
@@ -2192,6 +2210,7 @@ extern "C" int hh_decode_device_async(hh_decoder *d, const void *d_data, uint64_
     d->apend.d_out = d_out;
     d->apend.out_len = out_len;
     d->apend.st = st;
+    d->apend.ro = nullptr;
     d->async_seq++;
     return HH_OK;
 }
@@ -2258,6 +2277,55 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
                                &ro->const_seen, &ro->entry_state);
     ro->entry_exact = rg->prologue == 0 || cp != 0;
     return rc == HH_NOSYNC ? HH_ERR_UNSUPPORTED : rc;
+}
+
+// The asynchronous form (multi-GPU shards: a stream of segment decodes with
+// no host wait between them).  ro is filled when the decode is checked: by
+// the next asynchronous decode on this decoder or by hh_decode_wait.
+extern "C" int hh_decode_device_range_async(hh_decoder *d, const void *d_data, const hh_range *rg,
+                                            void *d_out, uint64_t cap, hh_range_out *ro,
+                                            void *hip_stream) {
+    if (!d || !rg || !ro || (!d_data && rg->bits_avail) || (!d_out && cap)) return HH_ERR_ARG;
+    if (!d->have_tree) return HH_ERR_ARG;
+    if (((uintptr_t)d_data & 3u) != 0) return HH_ERR_ARG;
+    if (!fsm_path_ok(d) || rg->bits_avail == 0 || rg->ntiles == 0) {
+        // (other paths, and empty segments: synchronously, as hh_decode_device_range)
+        async_check(d);
+        const int rc = hh_decode_device_range(d, d_data, rg, d_out, cap, ro, hip_stream);
+        if (rc != HH_OK && d->async_rc == HH_OK) d->async_rc = rc;
+        return rc == HH_ERR_CAPACITY ? HH_OK : rc;
+    }
+    if (rg->in_state >= d->fsm.ns) return HH_ERR_ARG;
+    hipStream_t st = (hipStream_t)hip_stream;
+    HIP_OK(hipSetDevice(d->device));
+    memset(ro, 0, sizeof(*ro));
+    ro->leave_state = ro->entry_state = rg->in_state;
+    // (known at launch: see hh_decode_device_range)
+    ro->const_seen = rg->ntiles > (uint64_t)d->fsm.cm;
+    ro->entry_exact = rg->prologue == 0;
+    const uint32_t slot = d->apend.active ? (d->apend.pd.slot ^ 1u) : 0u;
+    FsmPend pd;
+    memset(&pd, 0, sizeof(pd));
+    if (d->apend.active && !d->apend.fixed && d->apend.st != st)
+        HIP_OK(hipStreamWaitEvent(st, slot_ev(d, d->apend.pd.slot)[3], 0));
+    const int rc = fsm_launch(&d->fsm, &d->fsm_ws, slot, slot_ev(d, slot), d_data, rg->bits_avail, rg->ntiles,
+                              rg->in_state, rg->prologue, d_out, cap, st, &pd);
+    async_check(d);                     // the previous decode, while this one runs
+    if (rc != HH_OK) {
+        if (d->async_rc == HH_OK) d->async_rc = rc;
+        return rc;
+    }
+    d->apend.active = 1;
+    d->apend.fixed = 0;
+    d->apend.pd = pd;
+    d->apend.d_data = d_data;
+    d->apend.bits = rg->bits_avail;
+    d->apend.d_out = d_out;
+    d->apend.out_len = &ro->out_len;
+    d->apend.st = st;
+    d->apend.ro = ro;
+    d->async_seq++;
+    return HH_OK;
 }
 
 // evaluate() scope (decodeUtil.c:41-43 times the whole decoder call): host
@@ -2335,6 +2403,33 @@ static uint64_t pipe_chunk() {
     return v ? v : HH_PIPE_CHUNK;
 }
 
+// HH_FLAG_KEEP_HOST_PINNED: buffer k (0 payload, 1 output) page-locked
+// from p for at least n bytes, the registration kept for later calls
+static int pin_host(hh_decoder *d, int k, const void *p, size_t n) {
+    if (d->pin_p[k] == p && d->pin_n[k] >= n) return HH_OK;
+    if (d->pin_p[k]) (void)hipHostUnregister((void *)d->pin_p[k]);
+    d->pin_p[k] = nullptr;
+    d->pin_n[k] = 0;
+    // (the other buffer may be the same memory: then it is registered already)
+    if (d->pin_p[k ^ 1] && (const uint8_t *)p >= (const uint8_t *)d->pin_p[k ^ 1] &&
+        (const uint8_t *)p + n <= (const uint8_t *)d->pin_p[k ^ 1] + d->pin_n[k ^ 1])
+        return HH_OK;
+    if (hipHostRegister((void *)p, n, hipHostRegisterDefault) != hipSuccess) return HH_ERR_UNSUPPORTED;
+    d->pin_p[k] = p;
+    d->pin_n[k] = n;
+    return HH_OK;
+}
+
+extern "C" int hh_decoder_release_host(hh_decoder *d) {
+    if (!d) return HH_ERR_ARG;
+    for (int k = 0; k < 2; k++) {
+        if (d->pin_p[k]) (void)hipHostUnregister((void *)d->pin_p[k]);
+        d->pin_p[k] = nullptr;
+        d->pin_n[k] = 0;
+    }
+    return HH_OK;
+}
+
 static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint8_t *out, uint64_t cap,
                          uint64_t *out_len) {
     const uint64_t nb = (bits + 7) / 8;
@@ -2356,10 +2451,18 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
             d->npipe_ev = (uint32_t)(i + 1);
         }
     }
-    if (hipHostRegister((void *)data, nb, hipHostRegisterDefault) != hipSuccess) return HH_ERR_UNSUPPORTED;
-    if (cap && hipHostRegister(out, cap, hipHostRegisterDefault) != hipSuccess) {
-        (void)hipHostUnregister((void *)data);
-        return HH_ERR_UNSUPPORTED;
+    const bool keep = (d->cfg.flags & HH_FLAG_KEEP_HOST_PINNED) != 0;
+    if (keep) {
+        // the buffers stay registered across calls: (re)register only a new
+        // pointer or a longer length
+        if (pin_host(d, 0, data, nb) != HH_OK) return HH_ERR_UNSUPPORTED;
+        if (cap && pin_host(d, 1, out, cap) != HH_OK) return HH_ERR_UNSUPPORTED;
+    } else {
+        if (hipHostRegister((void *)data, nb, hipHostRegisterDefault) != hipSuccess) return HH_ERR_UNSUPPORTED;
+        if (cap && hipHostRegister(out, cap, hipHostRegisterDefault) != hipSuccess) {
+            (void)hipHostUnregister((void *)data);
+            return HH_ERR_UNSUPPORTED;
+        }
     }
     int rc = HH_OK;
     uint8_t *din = (uint8_t *)d->d_in, *dout = (uint8_t *)d->d_out;
@@ -2407,8 +2510,10 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
     }
     if (over && !rc) rc = HH_ERR_CAPACITY;
     if (hipStreamSynchronize(d->d2h) != hipSuccess || hipStreamSynchronize(d->h2d) != hipSuccess) rc = rc ? rc : HH_ERR_DEVICE;
-    (void)hipHostUnregister((void *)data);
-    if (cap) (void)hipHostUnregister(out);
+    if (!keep) {
+        (void)hipHostUnregister((void *)data);
+        if (cap) (void)hipHostUnregister(out);
+    }
     fsm_stats(d, bits, total, ms_all);
     *out_len = total;
     return rc == HH_NOSYNC ? HH_ERR_UNSUPPORTED : rc;   // (no resync: the serial path decodes it whole)

@@ -192,7 +192,9 @@ extern "C" int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_
     if (n == 0) return HH_OK;
     hipStream_t st = (hipStream_t)hip_stream;
     const uint64_t nch = (n + ENC_CH - 1) / ENC_CH;
-    if (nch > 0x7fffffffull) return HH_ERR_UNSUPPORTED;
+    // (a launch's grid may not exceed 2^32 - 1 threads: about 2^24 chunks,
+    // 68.7 G symbols, with ENC_TB threads each)
+    if (nch * ENC_TB > 0xffffffffull) return HH_ERR_UNSUPPORTED;
     // workspace: the table, the chunks' bits / offsets, the total and the
     // absent-symbol flag -- kept across calls per device (grown when a call
     // needs more; one call at a time per process: a per-call allocation and

@@ -1609,6 +1609,7 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, 
     if (getenv("HH_EMF_SWZ")) fd->swz = atoi(getenv("HH_EMF_SWZ")) != 0;
     // (the swizzled staging rounds the tables and a tile's staging up to
     // 128 B: one staging of the largest tile output must still fit)
+    fd->test_nosync = getenv("HH_TEST_NOSYNC") && atoi(getenv("HH_TEST_NOSYNC")) != 0;
     if (fd->swz && ((uint64_t)((emf_tab_bytes(ns, F->K, F->r) + 127u) & ~127u) + ((tmax + 16u + 8u + 127u) & ~127ull) >
                     EMF_LDS || !fd->sco))
         fd->swz = 0;
@@ -1810,6 +1811,7 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
     pd->emit_from = emit_from;
     pd->cap = cap;
     pd->slot = slot;
+    pd->test_nosync = fd->test_nosync;
     return HH_OK;
 }
 
@@ -1835,7 +1837,7 @@ int fsm_collect(FsmWs *ws, hipEvent_t *ev, const FsmPend *pd, uint64_t *total, u
         ms[0] = ms[1] = ms[2] = 0.0f;
         (void)hipEventElapsedTime(&ms[3], ev[0], ev[3]);
     }
-    if (fl & FF_FAIL) return HH_NOSYNC;
+    if ((fl & FF_FAIL) || pd->test_nosync) return HH_NOSYNC;
     if (*total > cap) return HH_ERR_CAPACITY;
     return HH_OK;
 }

@@ -27,6 +27,8 @@ struct FsmDev {
     uint32_t sco;            // k_emf's static copy-out (the default; HH_EMF_SCO=0: the store loop)
     uint32_t swz;            // k_emf's swizzled staging: codes whose lengths differ by at most 1 bit
     uint64_t *dbg;           // HH_DIAG builds: phase cycles of k_cnt (16 x u64, the decoder's)
+    uint32_t test_nosync;    // tests only (HH_TEST_NOSYNC=1 at set_tree): every decode reports chains
+                             // that did not meet, so that the callers' exact fallbacks run
 };
 
 // One decode of tiles [0, ntiles) of the segment at d_data (bits readable
@@ -51,7 +53,7 @@ struct FsmWs {
 // What fsm_collect needs of a decode fsm_launch enqueued.
 struct FsmPend {
     uint64_t nt, emit_from, cap;
-    uint32_t slot, phases;
+    uint32_t slot, phases, test_nosync;
 };
 void fsm_ws_free(FsmWs *ws);
 int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,

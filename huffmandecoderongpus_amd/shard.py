@@ -14,9 +14,16 @@ exchange (entry, leave, exactness, symbol count) -- 5 integers each, one
 all-gather -- which (a) proves every entry against the predecessor's leave
 state and lets a rank entered wrongly decode again with the right one (in
 at most world-1 more rounds; never needed when the prologue was exact), and
-(b) gives every rank its output base (exclusive sum of symbol counts).  The
-data path has no collective; assembling the global output is one all-gather
-of the decoded segments, timed separately (bench.py gather_report).
+(b) gives every rank its output base (exclusive sum of symbol counts).
+
+The exchange runs on a CHECKED step (check_step, before the timed region);
+the timed steps (decode_step) are the rank's decodes alone -- the prologue
+decode, plus the redo from the settled entry when the checked step needed
+one -- queued asynchronously, with no collective and no host wait; after
+the timed region one more exchange over the last timed step's results
+(confirm) must reproduce the checked step's rows.  The data path therefore
+has no collective; assembling the global output is one all-gather of the
+decoded segments, timed separately (bench.py gather_report).
 
 The settle protocol is pure Python over a `gather` callable so that it is
 tested with gloo on CPU (tests/test_shard.py) against the kernel's host
@@ -111,6 +118,38 @@ def settle(first: dict, redo, gather, rank: int, world: int) -> tuple[dict, list
     raise RuntimeError("shard entry states did not settle")
 
 
+def check_settle(first: dict, redo, gather, rank: int, world: int):
+    """The checked step's exchange: settle(), plus the state this rank was
+    redone from (None: its first entry was right).  Returns (result, rows,
+    redo_state)."""
+    called = []
+
+    def rec(st):
+        called.append(st)
+        return redo(st)
+    res, rows = settle(first, rec, gather, rank, world)
+    return res, rows, (called[-1] if called else None)
+
+
+def confirm(first: dict, redone: dict, gather, rank: int, world: int, rows_ref: list) -> bool:
+    """After the timed steps: the settle exchange over the last timed step's
+    results -- `first` its prologue decode, `redone` {state: result} of the
+    redo it queued -- must end with the checked step's rows and ask for no
+    decode the timed step did not do.  Collective (every rank calls it)."""
+    missing = []
+
+    def redo(st):
+        if st in redone:
+            return redone[st]
+        missing.append(st)
+        return {"in_state": st, "leave_state": -1, "entry_exact": True, "const_seen": False, "out_len": -1}
+    try:
+        _, rows = settle(first, redo, gather, rank, world)
+    except RuntimeError:
+        return False
+    return not missing and [list(map(int, r)) for r in rows] == [list(map(int, r)) for r in rows_ref]
+
+
 def out_base(rows: list, rank: int) -> int:
     return int(sum(int(rows[r][4]) for r in range(rank)))
 
@@ -149,7 +188,7 @@ class ShardJob:
     rank decodes its tiles (bench.py --gpus N)."""
 
     def __init__(self, hf, text: np.ndarray, target_bytes: int, rank: int, world: int,
-                 local: int, probe: int = PROBE_TILES):
+                 local: int, probe: int = PROBE_TILES, wrong_entry: bool = False):
         import torch
         import torch.distributed as dist
         import huffmandecoderongpus_amd as H
@@ -174,7 +213,21 @@ class ShardJob:
         self.compressed_bytes = (s.owned_bits + 7) // 8
         self.decoded_bytes = 0
         self.rows = None
+        self.redo_state = None
+        self._last = None
         self._dist = dist
+        # tests: a rank without a prologue enters in a state known to be
+        # wrong (its true entry found by a prologue decode here), so that the
+        # exchange must catch it and the timed steps include the redo
+        self.guess = 0
+        if wrong_entry and s.prologue == 0 and s.t0 > 0 and s.t1 > s.t0:
+            k = min(PROBE_TILES, s.t0)
+            pro = synth.tiled_stream(hf, text, 0, device=self.dev, bit_offset=(s.t0 - k) * tb,
+                                     bits=min(total_bits - (s.t0 - k) * tb, (k + 2) * tb))
+            r = self.dec.decode_range_ptr(pro.data.data_ptr(), pro.bits, k + 1, 0, self.out.data_ptr(),
+                                          self.cap, self.stream.cuda_stream, prologue=k)
+            del pro
+            self.guess = 1 if r["entry_state"] == 0 else 0
 
     def _gather(self, vals):
         import torch
@@ -184,29 +237,68 @@ class ShardJob:
         self._dist.all_gather(allt, t)
         return [[int(v) for v in a.tolist()] for a in allt]
 
-    def _decode(self, in_state: int, prologue: int) -> dict:
+    def _args(self, prologue: int):
         s = self.seg
         skip = (s.prologue - prologue) * s.tile_bits          # bits, multiple of 32
         # (no owned tile, fewer tiles than ranks: ntiles 0, and the range
         # decode leaves the chain in the state it entered)
         nt = s.ntiles - (s.prologue - prologue) if s.t1 > s.t0 else 0
-        r = self.dec.decode_range_ptr(self.syn.data.data_ptr() + skip // 8,
-                                      s.bits_avail - skip, nt, in_state, self.out.data_ptr(),
-                                      self.cap, self.stream.cuda_stream, prologue=prologue)
+        return self.syn.data.data_ptr() + skip // 8, s.bits_avail - skip, nt
+
+    def _decode(self, in_state: int, prologue: int) -> dict:
+        ptr, bits, nt = self._args(prologue)
+        r = self.dec.decode_range_ptr(ptr, bits, nt, in_state, self.out.data_ptr(), self.cap,
+                                      self.stream.cuda_stream, prologue=prologue)
         r["in_state"] = r["entry_state"]
         return r
 
-    def decode_step(self) -> int:
-        """One decode of this rank's shard, entry states settled (timed)."""
+    def _launch(self, in_state: int, prologue: int):
+        ptr, bits, nt = self._args(prologue)
+        return self.dec.decode_range_async_ptr(ptr, bits, nt, in_state, self.out.data_ptr(), self.cap,
+                                               self.stream.cuda_stream, prologue=prologue)
+
+    def _first(self, r: dict) -> dict:
         s = self.seg
-        first = self._decode(0, s.prologue)
         if s.prologue == 0 and s.t0 > 0:
-            first["entry_exact"] = False      # no prologue: the entry is a guess
-        res, rows = settle(first, lambda st: self._decode(st, 0), self._gather,
-                           self.rank, self.world)
+            r["entry_exact"] = False          # no prologue: the entry is a guess
+        return r
+
+    def check_step(self) -> int:
+        """The checked decode of this rank's shard (before the timed region):
+        the decode, the entry-state exchange (settle), the redo of a wrong
+        entry.  Fixes what the timed steps decode."""
+        s = self.seg
+        first = self._first(self._decode(self.guess, s.prologue))
+        res, rows, self.redo_state = check_settle(first, lambda st: self._decode(st, 0), self._gather,
+                                                  self.rank, self.world)
         self.rows = rows
         self.decoded_bytes = res["out_len"]
         return res["out_len"]
+
+    def decode_step(self) -> None:
+        """One timed decode of this rank's shard: the prologue decode and, when
+        the checked step's exchange found this rank's entry wrong, the redo
+        from the settled entry -- queued asynchronously (the decoder checks
+        the previous one meanwhile); no collective, no host wait."""
+        first = self._launch(self.guess, self.seg.prologue)
+        redo = self._launch(self.redo_state, 0) if self.redo_state is not None else None
+        self._last = (first, redo)
+
+    def wait(self) -> None:
+        self.dec.wait()
+
+    def confirm(self) -> bool:
+        """After the timed region: the exchange over the last timed step's
+        results must reproduce the checked step's rows (shard.confirm)."""
+        self.dec.wait()
+        first = self._last[0].as_dict()
+        first["in_state"] = first["entry_state"]
+        redone = {}
+        if self._last[1] is not None:
+            r = self._last[1].as_dict()
+            r["in_state"] = r["entry_state"]
+            redone[self.redo_state] = r
+        return confirm(self._first(first), redone, self._gather, self.rank, self.world, self.rows)
 
     def verify(self) -> bool:
         """Output == the tiled text from this rank's global symbol index."""

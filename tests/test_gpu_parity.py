@@ -316,6 +316,44 @@ def test_evaluate_scope_pipeline(hh, files_dir, chunk_kb, mib, monkeypatch):
         dec.close()
 
 
+def test_evaluate_scope_keeps_buffers_pinned(hh, files_dir, monkeypatch):
+    """HH_FLAG_KEEP_HOST_PINNED: hh_decode_host registers the caller's
+    buffers once and reuses the registration -- repeated calls on the same
+    buffers, then a NEW output buffer (re-registered), then a longer payload
+    view of a new array, then release_host and another call: every output
+    equals the tiled text (64 MiB stream, 4 MiB chunks: the pipelined
+    path)."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    monkeypatch.setenv("HH_PIPE_CHUNK_KB", "4096")
+    hf, text = synth.load_source(files_dir, "kjv.txt")
+    syn = synth.tiled_stream(hf, text, 64 << 20)
+    host = syn.data[: syn.compressed_bytes].cpu().numpy()
+    dec = hh.Decoder(0, flags=hh.FLAG_KEEP_HOST_PINNED)
+    try:
+        dec.set_tree(syn.tree)
+        n = syn.decoded_bytes
+
+        def check(out, buf):
+            assert len(out) == n
+            assert synth.verify_tiled(torch.from_numpy(out).cuda(), syn)
+            assert (buf[n + 16:] == 0xAB).all()
+        buf = np.full(n + 64, 0xAB, np.uint8)
+        for _ in range(3):
+            buf[:n] = 0
+            check(dec.decode_host(host, syn.bits, n + 16, out=buf), buf)
+        buf2 = np.full(n + 64, 0xAB, np.uint8)          # another output buffer
+        check(dec.decode_host(host, syn.bits, n + 16, out=buf2), buf2)
+        host2 = np.concatenate([host, np.zeros(4096, np.uint8)])   # another payload array
+        check(dec.decode_host(host2, syn.bits, n + 16, out=buf2), buf2)
+        dec.release_host()
+        buf[:n] = 0
+        check(dec.decode_host(host, syn.bits, n + 16, out=buf), buf)
+        assert dec.stats()["state_machine"] == 1
+    finally:
+        dec.close()
+
+
 @pytest.mark.parametrize("env", [{"HH_FRONT_WALK": "2"}, {"HH_FRONT_WALK": "16"},
                                  {"HH_FRONT_WALK": "8192"}, {"HH_EMIT_XPT": "0"},
                                  {"HH_EMIT_XPT": "1"}, {"HH_EMIT_NW": "8"}])
@@ -820,7 +858,7 @@ def test_eight_shards_of_the_8gib_stream():
         torch.cuda.empty_cache()
 
 
-def _shard_rank(rank, world, port, mib, q, backend="gloo"):
+def _shard_rank(rank, world, port, mib, q, backend="gloo", probe=2):
     import torch
     import torch.distributed as dist
     import huffmandecoderongpus_amd as H
@@ -832,29 +870,39 @@ def _shard_rank(rank, world, port, mib, q, backend="gloo"):
                                 rank=rank, world_size=world)
         torch.cuda.set_device(0)
         hf, text = synth.load_source(os.path.join(ROOT, "files"))
-        job = shard.ShardJob(hf, text, mib << 20, rank, world, 0)
-        ok = True
-        for _ in range(2):
+        job = shard.ShardJob(hf, text, mib << 20, rank, world, 0, probe=probe, wrong_entry=probe == 0)
+        job.check_step()                     # the checked step: decode + exchange
+        torch.cuda.synchronize()
+        ok = job.verify()
+        job.out.fill_(0)
+        for _ in range(3):                   # timed steps: decodes only, queued
             job.decode_step()
-            torch.cuda.synchronize()
-            ok = ok and job.verify()
+        job.wait()
+        torch.cuda.synchronize()
+        ok = ok and job.verify()             # (the timed steps' output)
+        ok = ok and job.confirm()            # the exchange after them agrees
         rep = job.gather_report()            # the assembled stream (gloo: host tensors)
         ok = ok and rep["allgather"]["seams_ok"]
-        q.put((rank, ok, job.decoded_bytes, job.seg.prologue))
+        q.put((rank, ok, job.decoded_bytes, job.seg.prologue, job.redo_state))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001
-        q.put((rank, repr(e), 0, 0))
+        q.put((rank, repr(e), 0, 0, None))
 
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_shard_job_two_ranks_one_gpu():
-    """bench.py's multi-GPU path (ShardJob: shard plan, prologue entry,
-    settle exchange, per-rank verification against the tiled text, the
-    all-gather assembly checked on rank 0) with two processes sharing GPU 0
-    over gloo (RCCL needs distinct GPUs)."""
+@pytest.mark.parametrize("probe", [2, 0])
+def test_shard_job_two_ranks_one_gpu(probe):
+    """bench.py's multi-GPU path (ShardJob: shard plan, prologue entry, the
+    checked step's settle exchange, timed steps queued asynchronously with
+    no collective, the exchange after them confirming the checked rows,
+    per-rank verification against the tiled text, the all-gather assembly
+    checked on rank 0) with two processes sharing GPU 0 over gloo (RCCL
+    needs distinct GPUs).  probe 0: rank 1 has no prologue and enters in a
+    state known to be wrong (ShardJob wrong_entry): the checked step's
+    exchange must catch it and the timed steps must include its redo."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -863,16 +911,19 @@ def test_shard_job_two_ranks_one_gpu():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_shard_rank, args=(r, 2, port, 32, q)) for r in range(2)]
+    ps = [ctx.Process(target=_shard_rank, args=(r, 2, port, 32, q, "gloo", probe)) for r in range(2)]
     for p in ps:
         p.start()
-    got = sorted(q.get(timeout=300) for _ in ps)
+    got = sorted((q.get(timeout=300) for _ in ps), key=lambda g: g[0])
     for p in ps:
         p.join(timeout=60)
-    for rank, ok, n, pro in got:
+    for rank, ok, n, pro, redo in got:
         assert ok is True, (rank, ok)
         assert n > 0
-    assert got[1][3] > 0          # rank 1 decoded a prologue
+    if probe:
+        assert got[1][3] > 0 and got[1][4] is None    # rank 1 decoded a prologue, entry right
+    else:
+        assert got[1][3] == 0 and got[1][4] is not None   # guessed entry wrong: redone
 
 
 def test_shard_job_over_rccl_one_rank():
@@ -890,7 +941,7 @@ def test_shard_job_over_rccl_one_rank():
     q = ctx.Queue()
     p = ctx.Process(target=_shard_rank, args=(0, 1, port, 32, q, "nccl"))
     p.start()
-    rank, ok, n, pro = q.get(timeout=300)
+    rank, ok, n, pro, redo = q.get(timeout=300)
     p.join(timeout=60)
     assert ok is True, ok
     assert n > 0 and pro == 0
@@ -979,6 +1030,85 @@ def test_async_decodes(hh, files_dir):
     finally:
         for dec in decs.values():
             dec.close()
+
+
+def test_async_decodes_on_two_streams(hh, files_dir):
+    """Asynchronous decodes alternating between two torch streams on ONE
+    decoder (its workspace is shared): each decode must wait for the pending
+    one's emission before its count pass rewrites the records -- kjv.txt and
+    a 64 MiB tiled stream, alternately, eight decodes, every output and
+    length checked after the wait."""
+    import torch
+    from huffmandecoderongpus_amd import synth
+    path = os.path.join(files_dir, "kjv.txt.huff")
+    hf = hh.HuffFile.load(path)
+    ref = O.OracleHuff.load(path).chain_decode()
+    text = torch.from_numpy(ref.copy()).cuda()
+    syn = synth.tiled_stream(hf, ref, 64 << 20, device=torch.device("cuda", 0))
+    buf = np.zeros(((hf.bits + 7) // 8 + 64 + 3) // 4 * 4, np.uint8)
+    buf[: (hf.bits + 7) // 8] = hf.data[: (hf.bits + 7) // 8]
+    small_in = torch.from_numpy(buf).cuda()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(hf.tree())
+        outs = [torch.full(((syn.decoded_bytes if k % 2 == 0 else len(ref)) + 4096,), 0xAB,
+                           dtype=torch.uint8, device="cuda") for k in range(8)]
+        torch.cuda.synchronize()          # (inputs and outputs made on the default stream)
+        pend = []
+        for k, out in enumerate(outs):
+            s = streams[k % 2]
+            if k % 2 == 0:
+                pend.append(("big", dec.decode_device_async(syn.data, syn.bits, out, s), out))
+            else:
+                pend.append(("small", dec.decode_device_async(small_in, hf.bits, out, s), out))
+        dec.wait()
+        torch.cuda.synchronize()
+        for kind, n, out in pend:
+            if kind == "big":
+                assert n.value == syn.decoded_bytes and synth.verify_tiled(out, syn)
+            else:
+                assert n.value == len(ref) and torch.equal(out[: n.value], text)
+            assert int(out[n.value: n.value + 64].ne(0xAB).sum()) == 0
+        assert dec.stats()["state_machine"] == 1
+    finally:
+        dec.close()
+        del syn
+        torch.cuda.empty_cache()
+
+
+def test_async_decode_exact_fallback(hh, files_dir, monkeypatch):
+    """The asynchronous path's exact fallback (async_check): a decode whose
+    chains are reported not to meet (HH_TEST_NOSYNC=1, the test hook that
+    makes every state-machine decode report it) is found failed while the
+    NEXT decode is already queued, and is decoded again on the segment path
+    through its saved arguments (output pointer, capacity, out_len pointer).
+    Three decodes of kjv.txt queued back to back into three buffers, then the
+    wait: every output and length equals the oracle's, and the fallback is
+    the segment path."""
+    import torch
+    monkeypatch.setenv("HH_TEST_NOSYNC", "1")
+    path = os.path.join(files_dir, "kjv.txt.huff")
+    hf = hh.HuffFile.load(path)
+    ref = O.OracleHuff.load(path).chain_decode()
+    buf = np.zeros(((hf.bits + 7) // 8 + 64 + 3) // 4 * 4, np.uint8)
+    buf[: (hf.bits + 7) // 8] = hf.data[: (hf.bits + 7) // 8]
+    d_in = torch.from_numpy(buf).cuda()
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(hf.tree())
+        outs = [torch.full((len(ref) + 4096,), 0xAB, dtype=torch.uint8, device="cuda") for _ in range(3)]
+        ns = [dec.decode_device_async(d_in, hf.bits, o) for o in outs]
+        dec.wait()
+        torch.cuda.synchronize()
+        st = dec.stats()
+        assert st["exact_fallback"] == 2 and st["repairs"] == 1
+        for n, o in zip(ns, outs):
+            assert n.value == len(ref)
+            assert np.array_equal(o[: n.value].cpu().numpy(), ref)
+            assert int(o[n.value: n.value + 64].ne(0xAB).sum()) == 0
+    finally:
+        dec.close()
 
 
 def test_non_resynchronising_code_takes_the_segment_path(hh):
@@ -1116,3 +1246,19 @@ def test_long_codes_beyond_2_31_bits(hh):
         dec.close()
         del out, payload, syms
         torch.cuda.empty_cache()
+
+
+def test_copy_probe(hh):
+    """hh_copy_device (bench.py's streaming-copy reference): both cache
+    policies copy every byte (an odd number of 16-B elements, not a multiple
+    of the kernel's stride), and a misaligned size is an argument error."""
+    import torch
+    n = (1 << 24) + 16 * 37
+    a = torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda")
+    for nt in (False, True):
+        b = torch.zeros_like(a)
+        ms = hh.copy_device(a, b, nt)
+        torch.cuda.synchronize()
+        assert ms > 0 and torch.equal(a, b)
+    with pytest.raises(hh.HipHuffError):
+        hh.copy_device(a[:17], torch.zeros(17, dtype=torch.uint8, device="cuda"))

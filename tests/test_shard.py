@@ -205,3 +205,74 @@ def test_gloo_shards_concatenate_to_the_stream(path, name, world, probe):
         assert redone == 0          # the prologue gives the exact entry
     elif path == "legacy" or name == "kjv.txt":
         assert redone >= 1
+
+
+def _confirm_worker(rank, world, port, probe, name, q):
+    import torch.distributed as dist
+    import torch
+    import huffmandecoderongpus_amd as H
+    from huffmandecoderongpus_amd import shard
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        hf = H.HuffFile.load(os.path.join(FILES, name + ".huff"))
+        tree = hf.tree()
+        L = _femu()
+        seg = shard.plan(hf.bits, 64 * FSM_S, world, rank, probe)
+
+        def gather(vals):
+            t = torch.tensor(vals, dtype=torch.int64)
+            allt = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(allt, t)
+            return [a.tolist() for a in allt]
+
+        def first_run():
+            r = femu_segment(L, tree, hf.payload, seg, 0, seg.prologue)
+            if seg.prologue == 0 and seg.t0 > 0:
+                r["entry_exact"] = False
+            return r
+        # the checked step: decode + exchange (+ redo)
+        res, rows, redo_state = shard.check_settle(
+            first_run(), lambda st: femu_segment(L, tree, hf.payload, seg, st, 0), gather, rank, world)
+        # a "timed" step: the same decodes, no exchange; then the confirming exchange
+        again = first_run()
+        redone = {} if redo_state is None else {redo_state: femu_segment(L, tree, hf.payload, seg, redo_state, 0)}
+        ok = shard.confirm(again, redone, gather, rank, world, rows)
+        # a timed step that skipped the redo it needed must not confirm
+        bad = shard.confirm(first_run(), {}, gather, rank, world, rows)
+        flags = [None] * world
+        dist.all_gather_object(flags, (ok, bad, redo_state is not None))
+        if rank == 0:
+            q.put(flags)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put(repr(e))
+        raise
+
+
+@pytest.mark.skipif(not os.path.exists(EMU), reason="tests/emu/libhh_emu.so not built")
+@pytest.mark.parametrize("world,probe", [(2, 2), (4, 0)])
+def test_gloo_timed_steps_without_exchange(world, probe):
+    """bench.py's multi-GPU step protocol (shard.check_settle / confirm) over
+    gloo with the state-machine emulation: the exchange runs on a checked
+    step, the timed steps repeat the decodes it fixed (the redo included),
+    and the exchange after them confirms the checked rows on every rank;
+    a timed step that left out a needed redo does not confirm.  probe 0:
+    ranks enter in a guessed state and some must be redone."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_confirm_worker, args=(r, world, port, probe, "kjv.txt", q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=240)
+    for p in ps:
+        p.join(timeout=60)
+    assert not isinstance(got, str), got
+    assert all(ok for ok, _, _ in got)
+    any_redo = any(r for _, _, r in got)
+    if probe:
+        assert not any_redo and all(bad for _, bad, _ in got)   # nothing to leave out
+    else:
+        assert any_redo and not any(bad for _, bad, _ in got)
