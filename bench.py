@@ -230,6 +230,30 @@ def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, s
             "state_machine_path": all(s["state_machine"] == 1 for s in st)}
 
 
+def gpu_local_cpus(device: int = 0):
+    """The host CPUs on the GPU's NUMA node that this process may run on
+    (None if unknown): hipDeviceGetPCIBusId -> /sys/bus/pci/devices/<id>/
+    local_cpulist, intersected with the process's affinity."""
+    import ctypes
+    try:
+        import torch  # noqa: F401  (its HIP runtime is the one loaded)
+        hip = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+            return None
+        bus = buf.value.decode().lower()
+        with open(f"/sys/bus/pci/devices/{bus}/local_cpulist") as f:
+            spec = f.read().strip()
+        cpus = set()
+        for part in spec.split(","):
+            a, _, b = part.partition("-")
+            cpus.update(range(int(a), int(b or a) + 1))
+        cpus &= os.sched_getaffinity(0)
+        return cpus or None
+    except (OSError, ValueError, AttributeError):
+        return None
+
+
 def evaluate_scope(H, hf, payload, bits: int, n_want: int, reps: int, check=None) -> dict:
     """The reference's evaluate() scope: the whole decoder call is timed
     (decodeUtil.c:41-43, 57-59) with the output buffer allocated and cleared
@@ -241,10 +265,19 @@ def evaluate_scope(H, hf, payload, bits: int, n_want: int, reps: int, check=None
     evaluate() reuses the same buffers for its 25 repeats) instead of
     registering ~3 GB in every call."""
     import numpy as np
+    # the caller's buffers on the GPU's NUMA node (first touch by a thread
+    # running there): DMA from the other socket's memory ran at about half
+    # the rate (68 against 39 ms per 1 GiB call in round 4's runs)
+    local = gpu_local_cpus(0)
+    keep_aff = os.sched_getaffinity(0)
+    if local:
+        os.sched_setaffinity(0, local)
+    payload = np.array(payload, np.uint8, copy=True)
     dec = H.Decoder(0, flags=H.FLAG_KEEP_HOST_PINNED)
     try:
         dec.set_tree(hf.tree())
         buf = np.zeros(n_want + 16, np.uint8)
+        buf[:] = 0
         out = dec.decode_host(payload, bits, n_want + 16, out=buf)   # first call: allocations
         ok = len(out) == n_want and (check is None or check(out))
         ts = []
@@ -258,9 +291,11 @@ def evaluate_scope(H, hf, payload, bits: int, n_want: int, reps: int, check=None
         return {"ok": bool(ok), "ms": round(ms, 3), "ms_min": round(min(ts) * 1e3, 3),
                 "ms_max": round(max(ts) * 1e3, 3),
                 "MBps": round(n_want / (ms * 1e-3) / 1e6, 1), "decoded_bytes": n_want, "reps": reps,
-                "host_buffers": "page-locked once, kept across calls (HH_FLAG_KEEP_HOST_PINNED)"}
+                "host_buffers": "page-locked once, kept across calls (HH_FLAG_KEEP_HOST_PINNED)",
+                "numa_local_cpus": len(local) if local else None}
     finally:
         dec.close()
+        os.sched_setaffinity(0, keep_aff)
 
 
 def encode_rate(H, hf, text, n: int, dev, reps: int = 5) -> dict:

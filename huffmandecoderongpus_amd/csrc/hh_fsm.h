@@ -32,14 +32,20 @@
  *   tsym[s]           the sym byte of the state's node: the symbol the
  *                     reference emits for a code cut off by the end of the
  *                     stream (its tail rule, decodeallbits.cl:20-31)
- *   et[s << K | v]    u64: K-bit steps (emission), v = the next K bits
+ *   et[s << LG | v]   u64: K-bit steps (emission), v = the next K bits;
+ *                     LG = HH_FSM_ET_LG(K) = max(K, 5) entries per state (K =
+ *                     4 rows are padded to 32 entries)
  *       bits  0..31   the symbols completed (first in bits 0..7, unused
  *                     bytes 0): K = 4..7 for codes of >= 2 bits, K = 4
  *                     when a code has 1 bit; a step from inside a code
  *                     completes up to 3 (K = 6) or 4 (K = 7, 4) symbols
- *       bits 32..39   8 x the number of symbols (the output shift)
- *       bits 47..63   the next state's row in et, in bytes: next << (K + 3)
- *                     (17 bits: K = 7 only for ns <= 127)
+ *       bits 32..37   8 x the number of symbols (the output shift; bits
+ *                     38..39 are 0)
+ *       bits 40..63   the next state's row in et, in bytes: next <<
+ *                     HH_FSM_ET_RSH(K) (= LG + 3 >= 8: the row bits of the
+ *                     high word start at bit 8, above the shift, so that the
+ *                     next entry's LDS address is one bit-field insert of the
+ *                     step's K bits, at bit 3, into the high word)
  *   er[s << r | v]    u64: the r-bit step that ends a region of S bits when K
  *                     does not divide S (r = S mod K, 0: none); same layout,
  *                     rows in et units
@@ -66,11 +72,13 @@ typedef struct {
     uint64_t er[HH_FSM_MAXS * 64];
 } hh_fsm_tables;
 
+#define HH_FSM_ET_LG(K) ((K) < 5u ? 5u : (K))          /* log2 entries per state row */
+#define HH_FSM_ET_RSH(K) (HH_FSM_ET_LG(K) + 3u)          /* log2 bytes per state row   */
 #define HH_FSM_ET_SYMS(e) ((uint32_t)(e))
-#define HH_FSM_ET_ROW(e) ((uint32_t)((e) >> 47))
-#define HH_FSM_ET_NSYM(e) ((uint32_t)((e) >> 35) & 31u)
+#define HH_FSM_ET_ROW(e) ((uint32_t)((e) >> 32) & ~255u)
+#define HH_FSM_ET_NSYM(e) (((uint32_t)((e) >> 32) & 255u) >> 3)
 #define HH_FSM_ET_MAKE(syms, row, n) \
-    ((uint64_t)(uint32_t)(syms) | (uint64_t)(8u * (uint32_t)(n)) << 32 | (uint64_t)(uint32_t)(row) << 47)
+    ((uint64_t)(uint32_t)(syms) | (uint64_t)((uint32_t)(row) | 8u * (uint32_t)(n)) << 32)
 #define HH_FSM_CT_NEXT(v, cb) ((uint32_t)(v) >> ((cb) + 1))
 #define HH_FSM_CT_CNT(v) ((uint32_t)(v) & 15u)
 

@@ -57,6 +57,9 @@
 #ifndef HH_CNT_IL
 #define HH_CNT_IL 0           // k_cnt: the next tile's heads interleaved with this tile's counts (measured no faster)
 #endif
+#ifndef HH_CNT_DADD
+#define HH_CNT_DADD 1         // k_cnt(m): a count step's entry added after the next step's read is issued
+#endif
 #ifndef HH_WALK_MASK
 #define HH_WALK_MASK 1        // k_cnt walks: only the lanes not met yet look up
 #endif
@@ -232,6 +235,23 @@ __device__ __forceinline__ uint32_t winsh(const uint32_t *w, uint32_t q) {
 // emission table
 template <uint32_t SW, uint32_t K>
 __device__ __forceinline__ uint32_t win8(const uint32_t *w, uint32_t q) { return winsh<SW, K, 3>(w, q); }
+// the same bits at bit 3 and up, the bits above them unmasked (the caller
+// inserts them with a bit-field insert)
+template <uint32_t SW, uint32_t K>
+__device__ __forceinline__ uint32_t win8raw(const uint32_t *w, uint32_t q) {
+    if (q < 3) return w[0] << (3 - q);
+    const uint32_t p = q - 3, i = p >> 5, o = p & 31;
+    if (o + K + 3 <= 32 || i + 1 >= SW) return w[i] >> o;
+    return __builtin_amdgcn_alignbit(w[i + 1], w[i], o);
+}
+// the LDS byte address of the emission entry for the step's K bits at q from
+// the high word of the previous entry (its row at bits >= 8, 8 x its symbols
+// at bits 3..5, bits 0..2 zero; hh_fsm.h): one bit-field insert
+template <uint32_t SW, uint32_t K>
+__device__ __forceinline__ uint32_t et_addr(uint32_t hi, const uint32_t *w, uint32_t q) {
+    constexpr uint32_t M = ((1u << K) - 1u) << 3;
+    return (win8raw<SW, K>(w, q) & M) | (hi & ~M);
+}
 // bit q of a region held in registers, q not a compile-time constant (rare paths)
 template <uint32_t SW>
 __device__ __forceinline__ uint32_t rbit_dyn(const uint32_t *w, uint32_t q) {
@@ -308,17 +328,26 @@ __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_
                                                uint32_t s, uint32_t lim, uint32_t *n, const uint32_t *wn = nullptr,
                                                uint32_t *hg = nullptr) {
     typedef HeadGeo<SW, CB> HG;
-    uint32_t c = 0, h = 0;
+    uint32_t c = 0, h = 0, ep = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 32 * SW / CB; k++) {
         if (!TAIL || CB * k + CB <= lim) {
             const uint32_t e = ct_at<CB>(lds, s, cstep<SW, CB>(w, k));
             s = e;
-            c += e;                              // (the counts: c's low RS bits, CntFmt::CM)
-            // (the entry added at its step: left to the scheduler, the adds
-            // sink to the end of the chain and every step's entry stays live
-            // -- 32 registers, the difference between 24 and 32 waves per CU)
-            asm volatile("" : "+v"(c));
+            // (the counts: c's low RS bits, CntFmt::CM.  Each entry is added
+            // one step late, after the next read is issued: the add is then
+            // off the chain's read -> AND-OR -> read path.  Added at its
+            // step but left to the scheduler, the adds sink to the end of
+            // the chain and every step's entry stays live -- 32 registers,
+            // the difference between 24 and 32 waves per CU)
+            if (HH_CNT_DADD) {
+                c += ep;
+                asm volatile("" : "+v"(c));
+                ep = e;
+            } else {
+                c += e;
+                asm volatile("" : "+v"(c));
+            }
         }
         if (IL) {
 #pragma unroll
@@ -335,6 +364,7 @@ __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_
         }
     }
     if (IL) *hg = h & CntFmt<CB>::RM;
+    if (HH_CNT_DADD) c += ep;
     c &= CntFmt<CB>::CM;
     s &= CntFmt<CB>::RM;
     if (TAIL)
@@ -1109,7 +1139,7 @@ __global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_
 // k_emf: emission of tiles [t0, t1), one tile per wave.
 // ---------------------------------------------------------------------------
 __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, uint32_t r) {
-    return ((ns << K) * 8u + (r ? (ns << r) * 8u : 0u) + ns * 8u + ns + 15u) & ~15u;
+    return ((ns << HH_FSM_ET_LG(K)) * 8u + (r ? (ns << r) * 8u : 0u) + ns * 8u + ns + 15u) & ~15u;
 }
 
 // The emission chain of one region (state, output dword, shift) while it
@@ -1120,12 +1150,6 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
 // neighbouring runs is repaired by OR afterwards (emf_edges).
 #ifndef HH_EMF_CPOL
 #define HH_EMF_CPOL 2         // k_emf's static copy-out stores: cache policy bits (2: nt -- 1 GiB kjv -3 % against plain)
-#endif
-#ifndef HH_EMF_STFULL
-#define HH_EMF_STFULL 1       // k_emf: a step stores its dword only when full (0: every step)
-#endif
-#ifndef EMF_KE
-#define EMF_KE 8          // steps within which the first dword is captured
 #endif
 // Staging swizzle (SWZ, near-uniform codes): the dword at LDS byte address a
 // is kept at a ^ (((a >> 7) & 31) << 2), i.e. dwords are permuted within
@@ -1156,21 +1180,37 @@ __device__ __forceinline__ u32x4 emf_read16(const uint8_t *lds, uint32_t a) {
     return o;
 }
 
+#ifndef HH_EMF_PUT64
+#define HH_EMF_PUT64 1        // k_emf: a step's bytes shifted into the current dword with one 64-bit shift
+#endif
+typedef uint32_t __attribute__((address_space(3))) *lds_u32p;
 template <uint32_t K, bool SWZ = false>
 struct EmfChain {
-    uint32_t row, wd0, wd, sh, a, fw, wdk;
+    uint32_t row, wd, sh, a;
     __device__ __forceinline__ void init(uint32_t s, uint32_t oa) {
-        row = s << (K + 3);
-        wd0 = oa & ~3u;
-        wd = wd0;
+        row = s << HH_FSM_ET_RSH(K);
+        wd = oa & ~3u;
         sh = (oa & 3u) * 8u;
         a = 0;                                      // the current dword's bytes so far
-        fw = 0;
-        wdk = wd0;
     }
     __device__ __forceinline__ uint32_t put(uint8_t *lds, uint64_t e) {
         const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
         const uint32_t u = sh + (hi & 255u);          // 8 x the symbols: one SDWA add
+        if (HH_EMF_PUT64) {
+            // one 64-bit shift gives both the bytes that fit the current
+            // dword and those that spill into the next (none at sh = 0): 2
+            // VALU instead of 5 (shift-or, negate, alignbit, compare, select);
+            // the store through an LDS-space pointer (the staging's byte
+            // address is its LDS address: no base add)
+            const uint64_t t = (uint64_t)lo << sh;
+            const uint32_t an = (uint32_t)t | a;
+            const bool full = u >= 32;
+            if (full) *(lds_u32p)(uintptr_t)emf_swz<SWZ>(wd) = an;
+            a = full ? (uint32_t)(t >> 32) : an;
+            wd += full ? 4u : 0u;
+            sh = u & 31u;
+            return an;
+        }
         // the bytes that do not fit the current dword spill into the next;
         // K = 6 (and 5) steps carry at most 3 symbols, so nothing spills at
         // sh = 0, K = 7 and K = 4 steps up to 4 (7 bits from inside a code:
@@ -1182,38 +1222,87 @@ struct EmfChain {
         // the dword once it is full (the run's last, partial one at the end):
         // an exec-masked store's LDS cycles count its active lanes' addresses
         // only, and a dword fills every 2.5 steps on kjv
-        if (!HH_EMF_STFULL || full) *(uint32_t *)(lds + emf_swz<SWZ>(wd)) = an;
+        if (full) *(uint32_t *)(lds + emf_swz<SWZ>(wd)) = an;
         a = full ? sp : an;
         wd += full ? 4u : 0u;
         sh = u & 31u;
         return an;
     }
-    // step k's entry e: store its symbols, capture the first dword, advance
-    __device__ __forceinline__ void step(uint8_t *lds, uint64_t e, uint32_t k) {
-        const uint32_t at = wd;
-        const uint32_t v = put(lds, e);
-        if (k < EMF_KE) fw = at == wd0 ? v : fw;     // the last value stored to the first dword
+    // a step's entry e: store its symbols, advance
+    __device__ __forceinline__ void step(uint8_t *lds, uint64_t e) {
+        put(lds, e);
         row = HH_FSM_ET_ROW(e);
-        if (k + 1 == EMF_KE) wdk = wd;
     }
 };
+#ifndef HH_EMF_PIPE
+#define HH_EMF_PIPE 1         // k_emf: step k+1's table read issued before step k's symbols are stored
+#endif
 
 // NCH independent regions (one per chain: region j of NCH tiles) entered in
 // states s[c], their symbols to the staging from LDS byte address oa[c] on:
 // K-bit steps, the NCH chains' table reads issued together (each chain is a
 // dependent sequence of LDS reads; interleaving them hides the latency), then
 // the r-bit step (r = S mod K); TAIL (NCH = 1): steps while whole, the rest
-// bit by bit, and the tail rule.  *first: the run's bytes in its first dword
-// (valid when *first_ok), *lastw / *lastwd: the run's last dword.
+// bit by bit, and the tail rule.
+//
+// Dwords shared between runs: a dword is stored, during the steps, only by
+// the run that fills its last byte (its value holds that run's bytes, zeros
+// where earlier runs' bytes go); the run that ends the tile stores its last,
+// partial dword at the end; every other run that ends inside a dword ORs its
+// bytes there after every lane's stores (emf_edges: *lastw at *lastwd when
+// *lastpart).  So every dword of the tile's output is stored exactly once
+// before the ORs, and no run's first dword needs capturing.
 template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SWZ = false>
 __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const uint32_t *b1, const uint8_t *ts,
                                            const uint32_t (*w)[SW], const uint32_t *s, uint32_t lim,
-                                           const bool *at_end, const uint32_t *oa, uint32_t *first, bool *first_ok,
-                                           uint32_t *lastw, uint32_t *lastwd) {
+                                           const bool *at_end, const uint32_t *oa, const bool *tlast,
+                                           uint32_t *lastw, uint32_t *lastwd, bool *lastpart) {
     constexpr uint32_t S = 32 * SW, r = S % K;
     EmfChain<K, SWZ> ch[NCH];
 #pragma unroll
     for (uint32_t c = 0; c < NCH; c++) ch[c].init(s[c], oa[c]);
+    constexpr uint32_t NST = S / K;
+    if (!TAIL && HH_EMF_PIPE) {
+        // The chain's critical path is read -> next row -> next read; the
+        // symbols' shifts, the full-dword test and the exec-masked store are
+        // off it.  Step k+1's read (and after the last step the remainder
+        // step's) is issued as soon as step k's entry is back, before step
+        // k's store logic: one wait per step, and the store work of a step
+        // overlaps the next read's latency (in program order the compiler
+        // put the whole store block between a read's return and the next read).
+        uint64_t e[NCH];
+#pragma unroll
+        for (uint32_t c = 0; c < NCH; c++) e[c] = *(const uint64_t *)(lds + et_addr<SW, K>(ch[c].row, w[c], 0));
+#pragma unroll
+        for (uint32_t k = 0; k < NST; k++) {
+            uint64_t en[NCH];
+#pragma unroll
+            for (uint32_t c = 0; c < NCH; c++) {
+                const uint32_t hi = (uint32_t)(e[c] >> 32);
+                if (k + 1 < NST) {
+                    en[c] = *(const uint64_t __attribute__((address_space(3))) *)(uintptr_t)et_addr<SW, K>(hi, w[c], (k + 1) * K);
+                } else if (r) {
+                    en[c] = *(const uint64_t *)(lds + er_off + (HH_FSM_ET_ROW(e[c]) >> (HH_FSM_ET_LG(K) - r)) +
+                                                (rbits<SW>(w[c], S - r, r) << 3));
+                } else {
+                    en[c] = 0;
+                }
+                ch[c].row = HH_FSM_ET_ROW(e[c]);
+            }
+#pragma unroll
+            for (uint32_t c = 0; c < NCH; c++) {
+                ch[c].put(lds, e[c]);
+                e[c] = en[c];
+            }
+        }
+        if (r) {
+#pragma unroll
+            for (uint32_t c = 0; c < NCH; c++) {
+                ch[c].put(lds, e[c]);
+                ch[c].row = HH_FSM_ET_ROW(e[c]);
+            }
+        }
+    } else {
 #pragma unroll
     for (uint32_t k = 0; k < S / K; k++) {
         const uint32_t q = k * K;
@@ -1222,65 +1311,41 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
 #pragma unroll
             for (uint32_t c = 0; c < NCH; c++) e[c] = *(const uint64_t *)(lds + ch[c].row + win8<SW, K>(w[c], q));
 #pragma unroll
-            for (uint32_t c = 0; c < NCH; c++) ch[c].step(lds, e[c], k);
-        } else if (k + 1 == EMF_KE) {
-#pragma unroll
-            for (uint32_t c = 0; c < NCH; c++) ch[c].wdk = ch[c].wd;
+            for (uint32_t c = 0; c < NCH; c++) ch[c].step(lds, e[c]);
         }
+    }
     }
 #pragma unroll
     for (uint32_t c = 0; c < NCH; c++) {
         EmfChain<K, SWZ> &x = ch[c];
         if (!TAIL) {
-            if (r) {
-                const uint64_t e = *(const uint64_t *)(lds + er_off + (x.row >> (K - r)) + (rbits<SW>(w[c], S - r, r) << 3));
+            if (r && !HH_EMF_PIPE) {
+                const uint64_t e = *(const uint64_t *)(lds + er_off + (x.row >> (HH_FSM_ET_LG(K) - r)) + (rbits<SW>(w[c], S - r, r) << 3));
                 x.put(lds, e);
                 x.row = HH_FSM_ET_ROW(e);
             }
         } else {
-            uint32_t st = x.row >> (K + 3);
+            uint32_t st = x.row >> HH_FSM_ET_RSH(K);
             for (uint32_t q = lim / K * K; q < lim; q++) {
                 const uint32_t v = b1[st * 2 + rbit_dyn<SW>(w[c], q)];
                 st = v & 255u;
                 x.put(lds, HH_FSM_ET_MAKE((v >> 16) & 255u, 0u, (v >> 8) & 255u));
             }
-            x.row = st << (K + 3);
+            x.row = st << HH_FSM_ET_RSH(K);
         }
-        if (at_end[c] && (x.row >> (K + 3)) != 0) x.put(lds, HH_FSM_ET_MAKE(ts[x.row >> (K + 3)], 0u, 1u));   // the tail rule
-        *(uint32_t *)(lds + emf_swz<SWZ>(x.wd)) = x.a;   // the bytes of the last step's overflow
-        // the first dword: complete in fw once the run left it within EMF_KE
-        // steps; the final dword when the run never left it
-        first[c] = x.wd == x.wd0 ? x.a : x.fw;
-        first_ok[c] = x.wd == x.wd0 || x.wdk != x.wd0 || (S / K < EMF_KE);
+        if (at_end[c] && (x.row >> HH_FSM_ET_RSH(K)) != 0) x.put(lds, HH_FSM_ET_MAKE(ts[x.row >> HH_FSM_ET_RSH(K)], 0u, 1u));   // the tail rule
+        if (tlast[c] && x.sh) *(uint32_t *)(lds + emf_swz<SWZ>(x.wd)) = x.a;   // the tile's last, partial dword
         lastw[c] = x.a;
         lastwd[c] = x.wd;
+        lastpart[c] = x.sh != 0 && !tlast[c];
     }
 }
 
-// After every lane's stores: the dwords a run shares with its neighbours hold
-// one run's bytes (and zeros); each run ORs its own bytes back into its first
-// and last dword.  The first dword's bytes were captured by emf_region (a
-// bit-serial re-run when the run left its first dword late).
-template <uint32_t SW, uint32_t K, bool SWZ = false>
-__device__ __forceinline__ void emf_edges(uint8_t *lds, const uint32_t *b1, const uint8_t *ts, const uint32_t *w,
-                                          uint32_t s, uint32_t lim, bool at_end, uint32_t cnt, uint32_t oa,
-                                          uint32_t first, bool first_ok, uint32_t lastw, uint32_t lastwd) {
-    if (!cnt) return;
-    const uint32_t b0 = oa & 3u;
-    uint32_t firstw = first;
-    if (!first_ok) {
-        const uint32_t need = 4u - b0 < cnt ? 4u - b0 : cnt;   // the run's bytes in its first dword
-        uint32_t acc = 0, got = 0, st = s;
-        for (uint32_t q = 0; q < lim && got < need; q++) {
-            const uint32_t v = b1[st * 2 + rbit_dyn<SW>(w, q)];
-            st = v & 255u;
-            if ((v >> 8) & 255u) acc |= ((v >> 16) & 255u) << (8 * got++);
-        }
-        if (got < need && at_end && st != 0) acc |= (uint32_t)ts[st] << (8 * got++);
-        firstw = acc << (8 * b0);
-    }
-    atomicOr((uint32_t *)(lds + emf_swz<SWZ>(oa & ~3u)), firstw);
-    if (lastwd != (oa & ~3u) && lastw) atomicOr((uint32_t *)(lds + emf_swz<SWZ>(lastwd)), lastw);
+// After every lane's stores (emf_region): a run that ends inside a dword ORs
+// its bytes into it (the run that fills the dword stored it with zeros there).
+template <bool SWZ = false>
+__device__ __forceinline__ void emf_edges(uint8_t *lds, uint32_t lastw, uint32_t lastwd, bool lastpart) {
+    if (lastpart) atomicOr((uint32_t *)(lds + emf_swz<SWZ>(lastwd)), lastw);
 }
 
 // A region whose tile's output does not fit the staging buffer: its symbols
@@ -1324,11 +1389,11 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     constexpr uint32_t S = 32 * SW;
     const uint32_t ns = geo.ns, r = geo.r, tid = threadIdx.x, j = tid & 63u;
     const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));   // (uniform: scalar tile index)
-    const uint32_t er_off = (ns << K) * 8u;
+    const uint32_t er_off = (ns << HH_FSM_ET_LG(K)) * 8u;
     uint32_t *s_b1 = (uint32_t *)(smem + er_off + (r ? (ns << r) * 8u : 0u));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
     constexpr uint32_t EW = emf_waves(NCH);
-    lds_fill16(smem, tab.et, (ns << K) * 8u);             // (ns x 2^K u64: a multiple of 16 B)
+    lds_fill16(smem, tab.et, (ns << HH_FSM_ET_LG(K)) * 8u);   // (ns x 2^LG u64: a multiple of 16 B)
     for (uint32_t i = tid; r && i < (ns << r); i += blockDim.x) ((uint64_t *)(smem + er_off))[i] = tab.er[i];
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
@@ -1417,16 +1482,18 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
                 oa[x] = tabb + (wv * NCH + x) * obw + (live[x] && fit[x] ? a0[x] + L[x] : 0u);
             }
             prefetch(t + NCH * nwv < t1 ? t + NCH * nwv : t);
-            uint32_t fw[NCH], lw[NCH], lwd[NCH];
-            bool fok[NCH];
+            uint32_t lw[NCH], lwd[NCH];
+            bool lpart[NCH], tl[NCH];
+    #pragma unroll
+            for (uint32_t x = 0; x < NCH; x++) tl[x] = live[x] && fit[x] && c[x] > 0 && L[x] + c[x] == Tout[x];
             WAVE_SYNC();                                  // the previous tiles' copy-out has read the staging
             EDIAG_STAMP(0);
-            emf_region<SW, K, TAIL, NCH, SWZ>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, fw, fok, lw, lwd);
+            emf_region<SW, K, TAIL, NCH, SWZ>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, tl, lw, lwd, lpart);
             WAVE_SYNC();
             EDIAG_STAMP(1);
     #pragma unroll
             for (uint32_t x = 0; x < NCH; x++)
-                if (live[x] && fit[x]) emf_edges<SW, K, SWZ>(smem, s_b1, s_ts, w[x], ent[x], lim, at_end[x], c[x], oa[x], fw[x], fok[x], lw[x], lwd[x]);
+                if (live[x] && fit[x]) emf_edges<SWZ>(smem, lw[x], lwd[x], lpart[x]);
             WAVE_SYNC();
             EDIAG_STAMP(2);
     #pragma unroll
@@ -1616,12 +1683,12 @@ int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, 
     FS_OK(hipMalloc(&fd->ct, (size_t)ns << (F->cb + 1)));
     FS_OK(hipMalloc(&fd->b1, (size_t)ns * 8));
     FS_OK(hipMalloc(&fd->tsym, (size_t)ns + 1));
-    FS_OK(hipMalloc(&fd->et, (size_t)(ns << F->K) * 8));
+    FS_OK(hipMalloc(&fd->et, (size_t)(ns << HH_FSM_ET_LG(F->K)) * 8));
     FS_OK(hipMalloc(&fd->er, (size_t)(ns << (F->r ? F->r : 1)) * 8));
     FS_OK(hipMemcpy(fd->ct, F->ct, (size_t)ns << (F->cb + 1), hipMemcpyHostToDevice));
     FS_OK(hipMemcpy(fd->b1, F->b1, (size_t)ns * 8, hipMemcpyHostToDevice));
     FS_OK(hipMemcpy(fd->tsym, F->tsym, (size_t)ns, hipMemcpyHostToDevice));
-    FS_OK(hipMemcpy(fd->et, F->et, (size_t)(ns << F->K) * 8, hipMemcpyHostToDevice));
+    FS_OK(hipMemcpy(fd->et, F->et, (size_t)(ns << HH_FSM_ET_LG(F->K)) * 8, hipMemcpyHostToDevice));
     if (F->r) FS_OK(hipMemcpy(fd->er, F->er, (size_t)(ns << F->r) * 8, hipMemcpyHostToDevice));
     fd->ok = 1;
     return HH_OK;

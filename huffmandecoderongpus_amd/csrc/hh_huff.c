@@ -511,14 +511,14 @@ int hh_fsm_build(const void *tv, uint32_t S, uint32_t Kreq, hh_fsm_tables *F) {
             const uint32_t to = fsm_walk(T, nd, bit, 1, 1, &sy, &n);
             F->b1[s * 2 + bit] = (uint32_t)st[to] | (n << 8) | (sy << 16);
         }
-        const uint32_t K = F->K;
+        const uint32_t K = F->K, LG = HH_FSM_ET_LG(K), RSH = HH_FSM_ET_RSH(K);
         for (uint32_t v = 0; v < (1u << K); v++) {
             const uint32_t to = fsm_walk(T, nd, v, K, 4, &sy, &n);
-            F->et[(s << K) | v] = HH_FSM_ET_MAKE(sy, (uint32_t)st[to] << (K + 3), n);
+            F->et[(s << LG) | v] = HH_FSM_ET_MAKE(sy, (uint32_t)st[to] << RSH, n);
         }
         for (uint32_t v = 0; F->r && v < (1u << F->r); v++) {
             const uint32_t to = fsm_walk(T, nd, v, F->r, 4, &sy, &n);
-            F->er[(s << F->r) | v] = HH_FSM_ET_MAKE(sy, (uint32_t)st[to] << (K + 3), n);
+            F->er[(s << F->r) | v] = HH_FSM_ET_MAKE(sy, (uint32_t)st[to] << RSH, n);
         }
     }
 out:

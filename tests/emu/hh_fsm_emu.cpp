@@ -172,7 +172,7 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
             uint32_t k = 0;
             if (R + S <= bits) {
                 // the kernels' fast path: K-bit steps, then the r-bit step
-                uint32_t row = e << (K + 3);
+                uint32_t row = e << HH_FSM_ET_RSH(K);
                 for (uint32_t q = 0; q + K <= S; q += K) {
                     const uint32_t v = (uint32_t)(((uint64_t)w[(R + q) >> 5] | (uint64_t)w[((R + q) >> 5) + 1] << 32) >>
                                                   ((R + q) & 31)) & ((1u << K) - 1u);
@@ -184,11 +184,11 @@ int64_t hh_fsm_emu_decode(const int32_t *izero, const int32_t *ione, const uint8
                     const uint64_t q = R + S - r;
                     const uint32_t v = (uint32_t)(((uint64_t)w[q >> 5] | (uint64_t)w[(q >> 5) + 1] << 32) >> (q & 31)) &
                                        ((1u << r) - 1u);
-                    const uint64_t en = g_F.er[((row >> (K + 3)) << r) + v];
+                    const uint64_t en = g_F.er[((row >> HH_FSM_ET_RSH(K)) << r) + v];
                     for (uint32_t i = 0; i < HH_FSM_ET_NSYM(en); i++) buf[k++] = (uint8_t)(HH_FSM_ET_SYMS(en) >> (8 * i));
                     row = HH_FSM_ET_ROW(en);
                 }
-                if (R + S == bits && (row >> (K + 3)) != 0) buf[k++] = g_F.tsym[row >> (K + 3)];   // tail rule
+                if (R + S == bits && (row >> HH_FSM_ET_RSH(K)) != 0) buf[k++] = g_F.tsym[row >> HH_FSM_ET_RSH(K)];   // tail rule
                 stats[7]++;
             } else {
                 k = fsm_emit_serial(&F, w, R, R + S, bits, e, buf);

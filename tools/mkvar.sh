@@ -9,6 +9,6 @@ F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-unused-result -Wno-unused-val
 /opt/rocm/bin/hipcc $F -c huffmandecoderongpus_amd/csrc/hh_device.hip -o $D/hh_device.o &
 /opt/rocm/bin/hipcc $F -c huffmandecoderongpus_amd/csrc/hh_fsm.hip -o $D/hh_fsm.o &
 wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o build/var/$N.so $D/hh_device.o $D/hh_fsm.o build/hh_huff.o build/hh_plugin.o build/hh_encode.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o build/var/$N.so $D/hh_device.o $D/hh_fsm.o build/hh_huff.o build/hh_plugin.o build/hh_encode.o build/hh_probe.o
 rm -rf $D
 echo build/var/$N.so

@@ -26,7 +26,7 @@ else:
 syn = synth.tiled_stream(hf, text, mib << 20)
 host = syn.data[: syn.compressed_bytes].cpu().numpy()
 n = syn.decoded_bytes
-dec = H.Decoder(0)
+dec = H.Decoder(0, flags=int(os.environ.get("HH_EVAL_FLAGS", "0")))
 dec.set_tree(syn.tree)
 buf = np.zeros(n + 16, np.uint8)
 out = dec.decode_host(host, syn.bits, n + 16, out=buf)
@@ -37,6 +37,33 @@ for _ in range(reps):
     t0 = time.perf_counter()
     dec.decode_host(host, syn.bits, n + 16, out=buf)
     ts.append(time.perf_counter() - t0)
-print(json.dumps({"lib": os.path.basename(os.environ.get("HIPHUFF_LIB", H.LIB_PATH)), "mib": mib, "ok": bool(ok),
-                  "ms": round(statistics.median(ts) * 1e3, 2), "ms_min": round(min(ts) * 1e3, 2),
-                  "chunk_kb": os.environ.get("HH_PIPE_CHUNK_KB")}))
+res = {"lib": os.path.basename(os.environ.get("HIPHUFF_LIB", H.LIB_PATH)), "mib": mib, "ok": bool(ok),
+       "flags": os.environ.get("HH_EVAL_FLAGS", "0"),
+       "ms": round(statistics.median(ts) * 1e3, 2), "ms_min": round(min(ts) * 1e3, 2),
+       "all_ms": [round(t * 1e3, 2) for t in ts], "chunk_kb": os.environ.get("HH_PIPE_CHUNK_KB")}
+if os.environ.get("HH_EVAL_DMA"):
+    # the PCIe floor: the same byte counts moved by plain async copies
+    # between pinned host tensors and the GPU, each way alone and both at once
+    hin = torch.from_numpy(host).pin_memory()
+    hout = torch.empty(n, dtype=torch.uint8).pin_memory()
+    din = torch.empty(hin.numel(), dtype=torch.uint8, device="cuda")
+    dout = torch.empty(n, dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def t(f):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        f()
+        torch.cuda.synchronize()
+        return round((time.perf_counter() - t0) * 1e3, 2)
+    for _ in range(2):
+        res["dma_h2d_ms"] = t(lambda: din.copy_(hin, non_blocking=True))
+        res["dma_d2h_ms"] = t(lambda: hout.copy_(dout, non_blocking=True))
+
+        def both():
+            with torch.cuda.stream(s1):
+                din.copy_(hin, non_blocking=True)
+            with torch.cuda.stream(s2):
+                hout.copy_(dout, non_blocking=True)
+        res["dma_both_ms"] = t(both)
+print(json.dumps(res))
