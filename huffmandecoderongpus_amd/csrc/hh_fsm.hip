@@ -118,6 +118,7 @@ struct FsmWork {
     int32_t *tsum;        // [ntiles] the tile's count (its own view of region 0)
     uint32_t *xs;         // [ntiles] the state leaving the tile
     uint32_t *fx;         // [ntiles + 1][FX_W] corrections of a tile's first regions
+    int32_t *fxs;         // [ntiles + 1] the sum of a tile's corrections (k_fscan1's view of fx)
     int32_t *lex;         // [ntiles + 1] exclusive prefix within the scan block
     int64_t *blk;         // [nblk] block totals, then block bases
     int32_t *bmax;        // [nblk] the block's largest tile count (k_emf sizes its staging by it)
@@ -589,6 +590,7 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
     // the next tile's corrections (its region 0 assumed entered in the head
     // guess, lane 63's gs); lanes j and j + 8k store the same word
     uint32_t fxv = 0, fail = 0;
+    int32_t fsum = 0;                               // (the corrections' sum: k_fscan1 reads it alone)
     if (has_next) {
         const bool lst = __builtin_amdgcn_readlane((int)lost, 63) != 0;
         if (!lst) {
@@ -597,6 +599,7 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
             const uint32_t g63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
             const bool walked = E63 != g63 || d63 != 0;      // (lane 63 walked into the next tile)
             fxv = (j & (FX_W - 1)) == 0 && walked ? fsm_fx(E63, d63) : 0u;
+            fsum = walked ? d63 : 0;
         } else {
             // rare: the chains meet beyond the next tile's region 0 (lane 0,
             // words from global memory)
@@ -609,11 +612,13 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
             for (int i = 0; i < FX_W; i++) {
                 const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)f[i], 0);
                 fxv = (j & (FX_W - 1)) == (uint32_t)i ? v : fxv;
+                fsum += fsm_fx_d(v);
             }
             fail = __builtin_amdgcn_readlane((int)ok, 0) ? 0u : 1u;
         }
     }
     wk.fx[(t + 1) * FX_W + (j & (FX_W - 1))] = fxv;   // ((ntiles + 1) x FX_W words: the last tile's too)
+    wk.fxs[t + 1] = fsum;
     wk.xs[t] = x | fail << 31;                        // (bit 31: chains that did not meet, k_fscan reports it)
     return (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
     CDIAG_STAMP(3);
@@ -673,6 +678,7 @@ __device__ __forceinline__ void cnt_run(const uint32_t *__restrict__ g, const Fs
     };
     CDIAG_DECL
     if (t == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
+    if (t == 0 && j == 0) wk.fxs[0] = 0;
     if (!TAIL && HH_CNT_IL && !HH_CNT_PNX && geo.G == CB * HeadGeo<SW, CB>::HS) {
         // Interleaved heads: tile t+1's heads run beside tile t's counts, so
         // a lane has two independent chains of lookups in flight.  The head
@@ -904,6 +910,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         }
     };
     if (c == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
+    if (c == 0 && j == 0) wk.fxs[0] = 0;
     if (c >= cend) return;
     c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
     // a lane's M regions are adjacent in memory (M * SW words): loaded in one
@@ -1010,6 +1017,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         wk.tsum[(uint64_t)c * M + grp] = v;
         const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)X, 63) >> RS;
         uint32_t fxv = 0, fail = 0;
+        int32_t fsum = 0;
         if (has_next) {
             const bool lst = __builtin_amdgcn_readlane((int)lost, 63) != 0;
             if (!lst) {
@@ -1018,6 +1026,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
                 const uint32_t g63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
                 const bool walked = E63 != g63 || d63 != 0;
                 fxv = (j & (FX_W - 1)) == 0 && walked ? fsm_fx(E63, d63) : 0u;
+                fsum = walked ? d63 : 0;
             } else {
                 uint32_t f[FX_W], ok = 1;
                 const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
@@ -1028,6 +1037,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
                 for (int i = 0; i < FX_W; i++) {
                     const uint32_t fv = (uint32_t)__builtin_amdgcn_readlane((int)f[i], 0);
                     fxv = (j & (FX_W - 1)) == (uint32_t)i ? fv : fxv;
+                    fsum += fsm_fx_d(fv);
                 }
                 fail = __builtin_amdgcn_readlane((int)ok, 0) ? 0u : 1u;
             }
@@ -1036,6 +1046,9 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         // emission tiles after its first (lanes 8 .. 8 M - 1)
         wk.fx[((uint64_t)c + 1) * M * FX_W + (j & (FX_W - 1))] = fxv;
         if (j < (M - 1) * FX_W) wk.fx[((uint64_t)c * M + 1) * FX_W + j] = 0u;
+        // (the sums: the next count tile's first emission tile, zero for this
+        // count tile's later ones)
+        wk.fxs[j < M ? (j == 0 ? ((uint64_t)c + 1) * M : (uint64_t)c * M + j) : ((uint64_t)c + 1) * M] = j == 0 || j >= M ? fsum : 0;
         // states leaving the emission tiles (the last one's is the tile's)
         wk.xs[(uint64_t)c * M + grp] = (grp == M - 1 ? x : 0u) | fail << 31;
         hin = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
@@ -1043,56 +1056,29 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
 }
 
 // ---------------------------------------------------------------------------
-// k_fscan1 / k_fscan2: output base of every tile
+// k_fscan1: output base of every tile
 // ---------------------------------------------------------------------------
-// One thread per tile t in [0, ntiles]: the tile's count (its own view plus
-// the corrections its predecessor wrote; prologue tiles emit nothing), the
-// exclusive prefix within the block -> lex, the block total -> blk.
-__global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk) {
-    __shared__ int32_t s_tmp[SCAN_TB / 64], s_mx[SCAN_TB / 64];
-    const uint64_t t = (uint64_t)blockIdx.x * SCAN_TB + threadIdx.x;
-    int32_t c = 0;
-    if (t < geo.ntiles && t >= geo.emit_from) {
-        c = wk.tsum[t];
-#pragma unroll
-        for (int i = 0; i < FX_W; i++) c += fsm_fx_d(wk.fx[t * FX_W + i]);
-    }
-    // a tile whose last chain met no other within HH_FSM_KM regions (k_cnt
-    // marks its leaving state)
-    if (__ballot(t < geo.ntiles && (wk.xs[t] >> 31)) && (threadIdx.x & 63u) == 0) atomicOr(wk.flags, (uint32_t)FF_FAIL);
-    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-    const int32_t x = wave_incl_scan(c);
-    int32_t m = c;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
-    if (lane == 63) s_tmp[wv] = x;
-    if (lane == 0) s_mx[wv] = m;
-    __syncthreads();
-    int32_t base = 0, tot = 0, mx = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < SCAN_TB / 64; i++) {
-        const int32_t v = s_tmp[i];
-        base += i < wv ? v : 0;
-        tot += v;
-        mx = max(mx, s_mx[i]);
-    }
-    if (t <= geo.ntiles) wk.lex[t] = base + x - c;
-    if (threadIdx.x == 0) {
-        wk.blk[blockIdx.x] = tot;
-        wk.bmax[blockIdx.x] = mx;
-    }
-}
-
-// One block: block totals -> exclusive block bases; totals and states.
-__global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_t nblk, uint32_t *res) {
+#define BMAX_FAIL 0x40000000    // bmax[b]: a tile of block b whose last chain met no other
+// The block totals -> exclusive block bases; totals and states into the
+// result slot (k_fscan1's last block; blk / bmax were stored sc1 by every
+// block, so they are read with sc1 loads -- agent-scope atomic loads -- and
+// no cache write-back or invalidate is needed on either side).
+__device__ void fscan_final(const FsmGeo &geo, const FsmWork &wk, uint32_t nblk, uint32_t *res) {
     __shared__ int64_t s_w[16];
-    __shared__ int32_t s_mx[16];
+    __shared__ int32_t s_mx2[16];
+    __shared__ uint32_t s_fl[16];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     int64_t carry = 0;
     int32_t mx = 0;
+    uint32_t fail = 0;
     for (uint32_t b0 = 0; b0 < nblk; b0 += 1024) {
-        const int64_t v = b0 + tid < nblk ? wk.blk[b0 + tid] : 0;
-        if (b0 + tid < nblk) mx = max(mx, wk.bmax[b0 + tid]);
+        int64_t v = 0;
+        if (b0 + tid < nblk) {
+            v = __hip_atomic_load(&wk.blk[b0 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int32_t bm = __hip_atomic_load(&wk.bmax[b0 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            mx = max(mx, bm & ~BMAX_FAIL);
+            fail |= (uint32_t)bm & BMAX_FAIL;
+        }
         int64_t x = v;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -1106,19 +1092,28 @@ __global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_
             base += i < wv ? s_w[i] : 0;
             tot += s_w[i];
         }
-        if (b0 + tid < nblk) wk.blk[b0 + tid] = carry + base + x - v;
+        if (b0 + tid < nblk) wk.blk[b0 + tid] = carry + base + x - v;   // (read by k_emf, after this kernel)
         carry += tot;
         __syncthreads();
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-    if (lane == 0) s_mx[wv] = mx;
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = max(mx, __shfl_xor(mx, o, 64));
+        fail |= (uint32_t)__shfl_xor((int)fail, o, 64);
+    }
+    if (lane == 0) {
+        s_mx2[wv] = mx;
+        s_fl[wv] = fail;
+    }
     __syncthreads();
     if (tid == 0) {
-        for (uint32_t i = 0; i < 16; i++) mx = max(mx, s_mx[i]);
+        uint32_t fl = 0;
+        for (uint32_t i = 0; i < 16; i++) {
+            mx = max(mx, s_mx2[i]);
+            fl |= s_fl[i] ? (uint32_t)FF_FAIL : 0u;
+        }
         wk.flags[6] = (uint32_t)mx;       // the largest tile output (symbols)
-        const uint32_t fl = wk.flags[0];
-        wk.flags[0] = 0u;                 // (k_fscan1's status of this decode read: cleared for the next)
+        wk.flags[8] = 0u;                 // (the block ticket, for the next decode's k_fscan1)
         const uint32_t lv = geo.ntiles ? wk.xs[geo.ntiles - 1] & 255u : geo.in_state;
         uint32_t en = geo.in_state;
         if (geo.emit_from < geo.ntiles) {
@@ -1133,6 +1128,51 @@ __global__ __launch_bounds__(1024) void k_fscan2(FsmGeo geo, FsmWork wk, uint32_
         res[5] = en;
         res[6] = (uint32_t)mx;
     }
+}
+
+// One thread per tile t in [0, ntiles]: the tile's count (its own view plus
+// the sum of the corrections its predecessor wrote; prologue tiles emit
+// nothing), the exclusive prefix within the block -> lex, the block total ->
+// blk.  The block that finishes last then scans the block totals
+// (fscan_final): one launch for the whole scan.  The hand-off without fences
+// (MI355X_MICROARCH.md, the sc1 hand-off table, row 1): each block's totals
+// stored sc1 by one lane, that lane's vmcnt(0), then its agent-scope add to
+// a ticket (flags[8]); the block whose add returns nblk - 1 reads them sc1.
+__global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk, uint32_t nblk, uint32_t *res) {
+    __shared__ int32_t s_tmp[SCAN_TB / 64], s_mx[SCAN_TB / 64];
+    __shared__ uint32_t s_last;
+    const uint64_t t = (uint64_t)blockIdx.x * SCAN_TB + threadIdx.x;
+    int32_t c = 0;
+    if (t < geo.ntiles && t >= geo.emit_from) c = wk.tsum[t] + wk.fxs[t];
+    // a tile whose last chain met no other within HH_FSM_KM regions (k_cnt
+    // marks its leaving state)
+    const bool fl = __ballot(t < geo.ntiles && (wk.xs[t] >> 31)) != 0;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    const int32_t x = wave_incl_scan(c);
+    int32_t m = c;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if (lane == 63) s_tmp[wv] = x;
+    if (lane == 0) s_mx[wv] = m | (fl ? BMAX_FAIL : 0);
+    __syncthreads();
+    int32_t base = 0, tot = 0, mx = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < SCAN_TB / 64; i++) {
+        const int32_t v = s_tmp[i];
+        base += i < wv ? v : 0;
+        tot += v;
+        mx = max(mx & ~BMAX_FAIL, s_mx[i] & ~BMAX_FAIL) | ((mx | s_mx[i]) & BMAX_FAIL);
+    }
+    if (t <= geo.ntiles) wk.lex[t] = base + x - c;
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&wk.blk[blockIdx.x], (int64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&wk.bmax[blockIdx.x], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = __hip_atomic_fetch_add(&wk.flags[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1u;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    fscan_final(geo, wk, nblk, res);
 }
 
 // ---------------------------------------------------------------------------
@@ -1180,6 +1220,12 @@ __device__ __forceinline__ u32x4 emf_read16(const uint8_t *lds, uint32_t a) {
     return o;
 }
 
+#ifndef HH_XP_HEADS
+#define HH_XP_HEADS 0         // (timing experiments only)
+#endif
+#ifndef HH_XP_TRANS
+#define HH_XP_TRANS 0         // (timing experiments only)
+#endif
 #ifndef HH_EMF_PUT64
 #define HH_EMF_PUT64 1        // k_emf: a step's bytes shifted into the current dword with one 64-bit shift
 #endif
@@ -1271,6 +1317,18 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
         // overlaps the next read's latency (in program order the compiler
         // put the whole store block between a read's return and the next read).
         uint64_t e[NCH];
+#if HH_XP_HEADS
+        // (single-pass cost experiment: a head chain of HH_XP_HEADS steps from
+        // the root over the region's words before its emission, as a single
+        // pass would run per region; the result kept alive, not used)
+        {
+            uint32_t hh = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < HH_XP_HEADS; k++)
+                hh = (uint32_t)(*(const uint64_t __attribute__((address_space(3))) *)(uintptr_t)et_addr<SW, K>(hh, w[0], (k * K) % (S - K)) >> 32);
+            asm volatile("" :: "v"(hh));
+        }
+#endif
 #pragma unroll
         for (uint32_t c = 0; c < NCH; c++) e[c] = *(const uint64_t *)(lds + et_addr<SW, K>(ch[c].row, w[c], 0));
 #pragma unroll
@@ -1365,7 +1423,7 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
 // k_emf: emission of tiles [t0, t1).  Each wave takes NCH tiles at a time
 // (tiles t, t + W, ..., W = the grid's active waves), one region of each per
 // lane.  The staging is sized from the largest tile output of this decode
-// (flags[6], k_fscan2): as many waves of the workgroup are active as the
+// (flags[6], k_fscan1's last block): as many waves of the workgroup are active as the
 // LDS beside the tables holds NCH tile stagings for (up to EW), so that
 // typical streams keep more chains in flight than a worst-case size allows.
 // SCO (static copy-out): the copy-out is COI unrolled lane-masked 16-B
@@ -1424,9 +1482,13 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
             for (uint32_t c = 0; c < NCH; c++) {
                 uint64_t tt = tt0 + c * nwv;
                 tt = uni64(tt < t1 ? tt : tt0);
-                const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tt * TB / 32, geo.nwords);
-                prec[c] = wk.rec[tt * NR + j];
-                pfx[c] = wk.fx[tt * FX_W + (j & (FX_W - 1))];
+#ifndef HH_XP_L2
+#define HH_XP_L2 0            // (timing experiments only: the first 64 tiles' words and records for every tile)
+#endif
+                const uint64_t tw = HH_XP_L2 ? (tt & 63u) : tt;
+                const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tw * TB / 32, geo.nwords);
+                prec[c] = wk.rec[tw * NR + j];
+                pfx[c] = wk.fx[tw * FX_W + (j & (FX_W - 1))];
                 const uint32_t *blk32 = (const uint32_t *)wk.blk + 2 * (tt / SCAN_TB);
                 const uint32_t ln = j & 3u;
                 pmeta[c] = *(ln == 0 ? blk32 : ln == 1 ? blk32 + 1 : (const uint32_t *)&wk.lex[tt]);
@@ -1494,6 +1556,23 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     #pragma unroll
             for (uint32_t x = 0; x < NCH; x++)
                 if (live[x] && fit[x]) emf_edges<SWZ>(smem, lw[x], lwd[x], lpart[x]);
+#if HH_XP_TRANS
+            // (single-pass cost experiment: a lane-column transposition -- each
+            // lane reads HH_XP_TRANS dwords of its run and writes them back,
+            // as moving lane columns into a contiguous staging would)
+            WAVE_SYNC();
+            {
+                const uint32_t b0 = oa[0] & ~3u, se = tabb + (wv * NCH + 1) * obw - 4u;   // (within the wave's slot)
+                uint32_t v[HH_XP_TRANS];
+#pragma unroll
+                for (uint32_t i = 0; i < HH_XP_TRANS; i++) v[i] = *(lds_u32p)(uintptr_t)min(b0 + 4 * i, se);
+                WAVE_SYNC();
+#pragma unroll
+                for (uint32_t i = 0; i < HH_XP_TRANS; i++) asm volatile("" : "+v"(v[i]));
+#pragma unroll
+                for (uint32_t i = 0; i < HH_XP_TRANS; i++) *(lds_u32p)(uintptr_t)min(b0 + 4 * i, se) = v[i];
+            }
+#endif
             WAVE_SYNC();
             EDIAG_STAMP(2);
     #pragma unroll
@@ -1585,6 +1664,7 @@ typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uin
 // 224-bit regions of trees of more than 127 states
 static kcntm_t kcntm_for(uint32_t sw, uint32_t cb, uint32_t m) {
     if (cb == 8 && sw == 8) return m == 2 ? k_cntm<8, 8, 2> : m == 4 ? k_cntm<8, 8, 4> : nullptr;
+    if (cb == 8 && sw == 7) return m == 2 ? k_cntm<7, 8, 2> : nullptr;   // 224-bit regions: 7-bit emission steps without a remainder
     if (cb == 7 && sw == HH_FSM_S7 / 32)
         return m == 2 ? k_cntm<HH_FSM_S7 / 32, 7, 2> : m == 4 ? k_cntm<HH_FSM_S7 / 32, 7, 4> : nullptr;
     return nullptr;
@@ -1601,10 +1681,16 @@ static kcnt_t kcnt_for(uint32_t sw, bool tail, uint32_t cb) {
     }
 }
 // chains per lane of the main emission launch
-static uint32_t emf_nch() { return 1u; }
+#ifndef HH_XP_EMF
+#define HH_XP_EMF 0           // (experiments: HH_EMF_NCH=2 chains per lane, HH_EMF_POOL staging bytes)
+#endif
+static uint32_t emf_nch() { return HH_XP_EMF && getenv("HH_EMF_NCH") ? (uint32_t)atoi(getenv("HH_EMF_NCH")) : 1u; }
 // (swz: the swizzled staging, with the static copy-out)
 static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sco, bool swz = false) {
     (void)nch;   // (two chains per lane: measured slower, not instantiated)
+#if HH_XP_EMF
+    if (nch == 2 && !tail && sw == 8 && K == 7 && sco && !swz) return k_emf<8, 7, false, 2, true>;
+#endif
     switch (sw) {
 #define EMF_K(n, k)                                                                                       \
     (tail ? k_emf<n, k, true, 1, false> : swz ? k_emf<n, k, false, 1, true, true>                         \
@@ -1738,7 +1824,7 @@ static int ws_need(FsmWs *ws, size_t need) {
     const size_t sz = need + need / 8;
     if (hipMalloc(&ws->p, sz) != hipSuccess) return HH_ERR_NOMEM;
     ws->size = sz;
-    FS_OK(hipMemset(ws->p, 0, 64));   // the status word; k_fscan2 clears it after each decode
+    FS_OK(hipMemset(ws->p, 0, 64));   // the status word and the scan's block ticket; k_fscan1's last block clears them
     return HH_OK;
 }
 
@@ -1759,7 +1845,7 @@ static int ws_side(FsmWs *ws) {
 }
 
 // The launch half: every kernel of the decode enqueued on st, the results
-// to be written by k_fscan2 into result slot `slot` of the host-mapped
+// to be written by k_fscan1's last block into result slot `slot` of the host-mapped
 // memory; *pd keeps what fsm_collect needs.
 int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void *d_data, uint64_t bits,
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap, hipStream_t st,
@@ -1783,9 +1869,10 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
     geo.emit_from = emit_from;
     const uint64_t nt = geo.ntiles;
     const uint32_t nblk = (uint32_t)((nt + 1 + SCAN_TB - 1) / SCAN_TB);
-    // workspace: flags 64 B | rec | tsum | xs | fx | lex | blk
+    // workspace: flags 64 B | rec | tsum | xs | fx | lex | fxs | blk
     const size_t o_rec = 64, o_tsum = o_rec + nt * NR * 4, o_xs = o_tsum + nt * 4, o_fx = o_xs + nt * 4;
-    const size_t o_lex = o_fx + (nt + 1) * FX_W * 4, o_blk = (o_lex + (nt + 1) * 4 + 7) & ~(size_t)7;
+    const size_t o_lex = o_fx + (nt + 1) * FX_W * 4, o_fxs = o_lex + (nt + 1) * 4;
+    const size_t o_blk = (o_fxs + (nt + 1) * 4 + 7) & ~(size_t)7;
     const size_t o_bmax = o_blk + (size_t)nblk * 8;
     rc = ws_need(ws, o_bmax + (size_t)nblk * 4);
     if (rc) return rc;
@@ -1797,6 +1884,7 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
     wk.xs = (uint32_t *)(w + o_xs);
     wk.fx = (uint32_t *)(w + o_fx);
     wk.lex = (int32_t *)(w + o_lex);
+    wk.fxs = (int32_t *)(w + o_fxs);
     wk.blk = (int64_t *)(w + o_blk);
     wk.bmax = (int32_t *)(w + o_bmax);
     wk.dbg = fd->dbg;
@@ -1845,9 +1933,7 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
         }
     }
     if (fd->phases) FS_OK(hipEventRecord(ev[1], st));
-    hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk);
-    FS_OK(hipGetLastError());
-    hipLaunchKernelGGL(k_fscan2, dim3(1), dim3(1024), 0, st, geo, wk, nblk, ws->d_res + 16 * slot);
+    hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk, nblk, ws->d_res + 16 * slot);
     FS_OK(hipGetLastError());
     if (fd->phases) FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
@@ -1861,9 +1947,11 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
             const uint64_t nwg = (ne - emit_from + ew - 1) / ew;
             const uint32_t gm = fd->grid_e > ntb + 1 ? fd->grid_e - ntb : 1u;
             const uint32_t ge = (uint32_t)(nwg < gm ? nwg : gm) + ntb;
+            uint32_t ldsb = (uint32_t)lds_emf(fd);
+            if (HH_XP_EMF && getenv("HH_EMF_POOL")) ldsb = emf_tab_bytes(fd->ns, fd->K, fd->r) + (uint32_t)atoi(getenv("HH_EMF_POOL"));
             hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch(), fd->sco, fd->swz), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne,
-                               (uint32_t)lds_emf(fd), ne, nt, ntb);
+                               ldsb, ne, nt, ntb);
             FS_OK(hipGetLastError());
         } else if (ne < nt) {
             hipLaunchKernelGGL(kemf_for(sw, fd->K, true, 1, false), dim3(ntb), dim3(64 * ew1), lds_emf(fd), st,

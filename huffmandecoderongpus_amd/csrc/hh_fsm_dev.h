@@ -44,7 +44,7 @@ struct FsmWs {
     void *p;
     size_t size;
     // the decode's results (status, total, leave / entry state), written by
-    // k_fscan2 straight into host-mapped memory: no copy, no memset per
+    // k_fscan1 (its last block) straight into host-mapped memory: no copy, no memset per
     // decode.  FSM_RES_SLOTS slots of 16 words: a decode in flight and the
     // next one enqueued behind it (hh_decode_device_async) keep theirs apart.
     uint32_t *h_res, *d_res;

@@ -1262,3 +1262,45 @@ def test_copy_probe(hh):
         assert ms > 0 and torch.equal(a, b)
     with pytest.raises(hh.HipHuffError):
         hh.copy_device(a[:17], torch.zeros(17, dtype=torch.uint8, device="cuda"))
+
+
+@pytest.mark.parametrize("nleaves,seed", [(300, 41), (500, 42)])
+def test_tree_beyond_the_state_machine_default_path(hh, nleaves, seed):
+    """A tree of more than 256 leaves (symbols repeat: the reference's loader
+    takes any node count, huffdata.c:41-54, and decodeallbits.cl:10-33 walks
+    any tree) has more than 255 internal nodes, past the state machine: the
+    DEFAULT decoder must still be exact -- random payload bits (every bit
+    string decodes with a complete tree) cut at several points, against the
+    oracle, through hh_decode_device and the evaluate() scope."""
+    rng = np.random.default_rng(seed)
+    izl, iol, leaves = [-1], [-1], [0]
+    while len(leaves) < nleaves:                    # random splits of random leaves
+        v = leaves.pop(int(rng.integers(len(leaves))))
+        a = len(izl)
+        izl[v], iol[v] = a, a + 1
+        izl += [-1, -1]
+        iol += [-1, -1]
+        leaves += [a, a + 1]
+    iz, io = np.array(izl), np.array(iol)
+    sy = rng.integers(0, 256, size=len(iz)).astype(np.uint8)     # repeated symbols
+    sy[iz != -1] = 0
+    t = hh.Tree(iz, io, sy)
+    info = t.info()
+    assert info["leaves"] == nleaves and nleaves - 1 > 255
+    nbytes = 400_000
+    data = rng.integers(0, 256, size=nbytes).astype(np.uint8)
+    dec = hh.Decoder(0)
+    try:
+        dec.set_tree(t)
+        for cut in (nbytes * 8, nbytes * 8 - 5, 123_457):
+            ref = _oracle(iz, io, sy, data, cut)
+            got = _decode_dev(hh, dec, data, cut, cut + 16)
+            st = dec.stats()
+            assert st["state_machine"] == 0
+            assert len(got) == len(ref) and np.array_equal(got, ref), (cut, st)
+        pay = np.zeros(nbytes + 64, np.uint8)
+        pay[:nbytes] = data
+        out = dec.decode_host(pay[:nbytes], nbytes * 8, nbytes * 8 + 16)
+        assert np.array_equal(out, _oracle(iz, io, sy, data, nbytes * 8))
+    finally:
+        dec.close()

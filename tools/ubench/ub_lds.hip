@@ -106,7 +106,15 @@ int main(int argc, char **argv) {
     uint32_t *h = (uint32_t *)calloc(NS * 1024, 1), *gt, *sink;
     CK(hipMalloc(&gt, NS * 1024));
     CK(hipMalloc(&sink, 64));
-    const int W[] = {4, 8, 12, 16, 24, 32};
+    if (argc > 2) {           // one configuration: rounds wpc ent (2 | 8), one chain per lane
+        const int wpc = atoi(argv[2]), ent = argc > 3 ? atoi(argv[3]) : 2;
+        fill(h, ent);
+        CK(hipMemcpy(gt, h, NS * (ent == 2 ? 512 : 1024), hipMemcpyHostToDevice));
+        if (ent == 2) run<2, 1>(ncu, gt, sink, wpc, rounds);
+        else run<8, 1>(ncu, gt, sink, wpc, rounds);
+        return 0;
+    }
+    const int W[] = {4, 8, 12, 16, 32};
     fill(h, 2);
     CK(hipMemcpy(gt, h, NS * 512, hipMemcpyHostToDevice));
     for (int w : W) run<2, 1>(ncu, gt, sink, w, rounds);
