@@ -44,6 +44,11 @@
 #include "hh_internal.h"
 #include "hiphuff.h"
 
+#ifdef HH_WSPAN
+#define HH_DBG_WORDS (16 + 6 * 8192)
+#else
+#define HH_DBG_WORDS 16
+#endif
 #define HH_MAXLEN_FAST 32           // longest code of the fast path (one cursor step <= 32 bits)
 // k_emit's waves per workgroup share one copy of the tables: 16 (one
 // workgroup per CU with the 12-bit L1, 32 KiB) when the tables fit beside
@@ -1481,7 +1486,7 @@ extern "C" int hh_decoder_create(hh_decoder **out, const hh_config *cfg) {
         hipMalloc(&d->d_tree, sizeof(uint32_t) * (HH_TREE_MAX + 1)) != hipSuccess ||
         hipMalloc(&d->d_tsym, HH_TREE_MAX + 1) != hipSuccess ||
         hipMalloc(&d->d_max, 16) != hipSuccess ||
-        hipMalloc(&d->d_dbg, 16 * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&d->d_dbg, HH_DBG_WORDS * sizeof(uint64_t)) != hipSuccess ||
         hipHostMalloc((void **)&d->h_flags, 64, hipHostMallocDefault) != hipSuccess) {
         hh_decoder_destroy(d);
         return HH_ERR_DEVICE;
@@ -2703,9 +2708,11 @@ extern "C" int hh_debug_failure(hh_decoder *d, uint32_t *out5) {
 // cycles summed over workgroups [0..3] (staging, pass 1, walks, table) and
 // walk statistics [8..11] (lanes, lookups, sum over waves of the wave's
 // longest walk, longest walk) of the last decode.
+// (HH_WSPAN builds: 16 + 6 x 8192 words -- the per-wave start / fill / end
+// stamps of k_cntm and k_emf after the 16 counters)
 extern "C" int hh_debug_counters(hh_decoder *d, uint64_t *out16) {
     if (!d || !out16) return HH_ERR_ARG;
-    if (hipMemcpy(out16, d->d_dbg, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(out16, d->d_dbg, HH_DBG_WORDS * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess)
         return HH_ERR_DEVICE;
     return HH_OK;
 }

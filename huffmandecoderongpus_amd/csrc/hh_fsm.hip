@@ -126,6 +126,23 @@ struct FsmWork {
                           // [8] tiles, [9] tiles with a walk, [10] walk rounds
 };
 
+// HH_WSPAN builds: when the waves of k_cntm (dbg[0..6]) and k_emf
+// (dbg[8..14]) start, finish their table fill and end, on the global
+// 100 MHz clock (s_memrealtime): max of ~start (-> earliest start), max
+// start, max of ~end, max end, sum of (end - start), waves, sum of (fill - start)
+#ifdef HH_WSPAN
+#define WSPAN_N 8192          // wave slots per kernel
+#define WSPAN_START(f) const uint64_t ws_t0_ = __builtin_amdgcn_s_memrealtime(); uint64_t ws_tf_ = ws_t0_; (void)(f)
+#define WSPAN_FILLED() ws_tf_ = __builtin_amdgcn_s_memrealtime()
+#define WSPAN_END(dbg, o) do { const uint64_t t1_ = __builtin_amdgcn_s_memrealtime(); \
+    const uint32_t w_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
+    if ((threadIdx.x & 63u) == 0 && (dbg) && w_ < WSPAN_N) { uint64_t *d_ = (dbg) + 16 + ((o) ? WSPAN_N * 3 : 0) + 3 * w_; \
+        d_[0] = ws_t0_; d_[1] = ws_tf_; d_[2] = t1_; } } while (0)
+#else
+#define WSPAN_START(f) do {} while (0)
+#define WSPAN_FILLED() do {} while (0)
+#define WSPAN_END(dbg, o) do {} while (0)
+#endif
 #ifdef HH_DIAG
 #define CDIAG_DECL uint64_t cg_acc[4] = {0, 0, 0, 0}, cg_n[3] = {0, 0, 0}; uint64_t cg_t = __builtin_amdgcn_s_memtime();
 #define CDIAG_STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); cg_acc[i] += t_ - cg_t; cg_t = t_; } while (0)
@@ -870,6 +887,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         cnt_run<SW, true, CB, CWM>(g, geo, tab, wk, u0, u1, blockIdx.x, ntb);
         return;
     }
+    WSPAN_START(0);
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS, LG = 64 / M;   // LG: lanes per emission tile
     constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
@@ -882,6 +900,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
     __syncthreads();
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts, CB};
+    WSPAN_FILLED();
     // each wave counts a contiguous run of count tiles, in order (lane 0's
     // entry guess of a tile: the previous tile's lane-63 head)
     const uint32_t nwv = (gridDim.x - ntb) * CWM, ce = (uint32_t)c1, gw = (blockIdx.x - ntb) * CWM + wv;
@@ -911,7 +930,10 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     };
     if (c == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
     if (c == 0 && j == 0) wk.fxs[0] = 0;
-    if (c >= cend) return;
+    if (c >= cend) {
+        WSPAN_END(wk.dbg, 0);
+        return;
+    }
     c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
     // a lane's M regions are adjacent in memory (M * SW words): loaded in one
     // burst, so that every cache line is read once and at once -- loaded a
@@ -1053,6 +1075,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         wk.xs[(uint64_t)c * M + grp] = (grp == M - 1 ? x : 0u) | fail << 31;
         hin = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
     }
+    WSPAN_END(wk.dbg, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1283,6 +1306,9 @@ struct EmfChain {
 #ifndef HH_EMF_PIPE
 #define HH_EMF_PIPE 1         // k_emf: step k+1's table read issued before step k's symbols are stored
 #endif
+#ifndef HH_EMF_DYN
+#define HH_EMF_DYN 1          // k_emf: the workgroup's tiles claimed one at a time from an LDS counter
+#endif
 
 // NCH independent regions (one per chain: region j of NCH tiles) entered in
 // states s[c], their symbols to the staging from LDS byte address oa[c] on:
@@ -1451,21 +1477,27 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     uint32_t *s_b1 = (uint32_t *)(smem + er_off + (r ? (ns << r) * 8u : 0u));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
     constexpr uint32_t EW = emf_waves(NCH);
+    WSPAN_START(0);
     lds_fill16(smem, tab.et, (ns << HH_FSM_ET_LG(K)) * 8u);   // (ns x 2^LG u64: a multiple of 16 B)
     for (uint32_t i = tid; r && i < (ns << r); i += blockDim.x) ((uint64_t *)(smem + er_off))[i] = tab.er[i];
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
+    // the workgroup's tile counter (DYN), in the LDS's last 16 bytes
+    constexpr bool DYN = !TAIL && NCH == 1 && HH_EMF_DYN;
+    const uint32_t ctr = lds_bytes - 16u;
+    if (DYN && tid == 0) *(lds_u32p)(uintptr_t)ctr = 0u;
     __syncthreads();
     // staging per tile: the largest tile output + its 16-B misalignment + the
     // last step's overflow dword; the active waves share the rest of the LDS
     const uint32_t tabb = SWZ ? (emf_tab_bytes(ns, K, r) + 127u) & ~127u : emf_tab_bytes(ns, K, r);   // (SWZ: 128-B chunks)
-    const uint32_t pool = lds_bytes > tabb ? lds_bytes - tabb : 0u;
+    const uint32_t pool = lds_bytes > tabb + 16u ? lds_bytes - tabb - 16u : 0u;
     const uint32_t mx = __builtin_amdgcn_readfirstlane((int)wk.flags[6]);
     constexpr uint32_t SU = SWZ ? 128u : 16u;         // staging slot unit (SWZ: whole 128-B chunks)
     const uint32_t need = (mx + 16u + 8u + SU - 1u) & ~(SU - 1u);
     uint32_t nact = pool / (NCH * need);
     nact = nact > EW ? EW : nact < 1u ? 1u : nact;
     if (nact > blockDim.x / 64u) nact = blockDim.x / 64u;
+    WSPAN_FILLED();
     if (wv >= nact) return;                          // (no workgroup barrier after this point)
     const uint32_t obw = pool / (NCH * nact) & ~(SU - 1u);   // (>= need: need is a multiple of SU)
 
@@ -1495,7 +1527,21 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
                 fs_load<SW>(pw[c], rs, j * SW);
             }
         };
-        uint64_t t = t0 + (uint64_t)blk * nact + wv;
+        // DYN: the workgroup's tiles t0 + k nwv + blk nact + v (v < nact), in
+        // the order u = k nact + v, go to its waves one at a time from the
+        // LDS counter -- with equal shares the workgroup's younger waves,
+        // behind the older ones in the SIMDs' issue order, ended up to 25 %
+        // later (per-wave end times, HH_WSPAN build)
+        auto tile_of = [&](uint32_t u) -> uint64_t {
+            const uint32_t k = u / nact;
+            return t0 + (uint64_t)k * nwv + (uint64_t)blk * nact + (u - k * nact);
+        };
+        auto claim = [&]() -> uint64_t {
+            uint32_t u = 0;
+            if (j == 0) u = __hip_atomic_fetch_add((lds_u32p)(uintptr_t)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return tile_of((uint32_t)__builtin_amdgcn_readlane((int)u, 0));
+        };
+        uint64_t t = DYN ? claim() : t0 + (uint64_t)blk * nact + wv, tn = t;
         EDIAG_DECL
         if (t < t1) prefetch(t);
         // (the first tile's loads complete here, once per wave: the compiler
@@ -1503,7 +1549,7 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
         // wait at the loop head, merged over both paths, was vmcnt(0) --
         // every tile waiting for the previous tile's stores)
         __builtin_amdgcn_s_waitcnt(VMCNT0);
-        for (; t < t1; t += NCH * nwv) {
+        for (; t < t1; t = tn) {
             uint32_t w[NCH][SW], ent[NCH], c[NCH], L[NCH], Tout[NCH], a0[NCH], oa[NCH], lim = S;
             uint64_t P0[NCH];
             bool at_end[NCH], fit[NCH], live[NCH];
@@ -1543,7 +1589,8 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
                 // all store at the slot's start, inside the slot)
                 oa[x] = tabb + (wv * NCH + x) * obw + (live[x] && fit[x] ? a0[x] + L[x] : 0u);
             }
-            prefetch(t + NCH * nwv < t1 ? t + NCH * nwv : t);
+            tn = DYN ? claim() : t + NCH * nwv;
+            prefetch(tn < t1 ? tn : t);
             uint32_t lw[NCH], lwd[NCH];
             bool lpart[NCH], tl[NCH];
     #pragma unroll
@@ -1633,6 +1680,7 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     else if (!TAIL && SCO && per <= 16) tiles(std::integral_constant<uint32_t, 16>{});
     else tiles(std::integral_constant<uint32_t, 0>{});
     EDIAG_FLUSH(wk.dbg);
+    if (!TAIL) WSPAN_END(wk.dbg, 8);
 }
 
 // k_emf: the emission of tiles [t0, t1); its first ntb workgroups (dispatched
@@ -1716,7 +1764,7 @@ static_assert(EMF_LDS <= 160u * 1024u, "k_emf's LDS");
 // output (k_emf sizes them at run time)
 bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile) {
     const uint64_t need = ((uint64_t)est_tile + 16u + 8u + 15u) & ~15ull;
-    return emf_tab_bytes(F->ns, F->K, F->r) + 16u * need <= EMF_LDS;
+    return emf_tab_bytes(F->ns, F->K, F->r) + 16u * need + 16u <= EMF_LDS;   // (+ k_emf's tile counter)
 }
 
 void fsm_free(FsmDev *fd) {
@@ -1890,8 +1938,11 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
     wk.dbg = fd->dbg;
     FsmTab tab = {fd->ct, fd->b1, fd->tsym, fd->et, fd->er};
     const uint32_t sw = fd->S / 32;
-#ifdef HH_DIAG
+#if defined(HH_DIAG)
     if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, 16 * sizeof(uint64_t), st));
+#endif
+#if defined(HH_WSPAN)
+    if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, (16 + 6 * WSPAN_N) * sizeof(uint64_t), st));
 #endif
     rc = ws_side(ws);
     if (rc) return rc;

@@ -74,7 +74,30 @@ res = {"lib": os.path.basename(os.environ.get("HIPHUFF_LIB", H.LIB_PATH)), "mib"
        "ok": bool(ok), "fast": dec.stats()["exact_fallback"] == 0}
 res.update({k: round(statistics.median(v), 4) for k, v in ph.items()})
 res["wall_ms"] = round(statistics.median(wall[1:]), 3)
-if os.environ.get("HH_DIAG") == "fsm":     # a -DHH_DIAG build: k_cnt phase cycles and walks
+if os.environ.get("HH_WSPAN"):             # a -DHH_WSPAN build: per-wave start / fill / end (100 MHz clock)
+    import ctypes as C
+    import numpy as np
+    N = 8192
+    buf = (C.c_uint64 * (16 + 6 * N))()
+    H.lib().hh_debug_counters(dec._h, buf)
+    a = np.ctypeslib.as_array(buf)[16:].astype(np.int64)
+    if os.environ.get("HH_WSPAN_DUMP"):
+        np.save(os.environ["HH_WSPAN_DUMP"] + f"_{mib}.npy", a)
+    for name, o in (("cnt", 0), ("emf", 3 * N)):
+        st = a[o:o + 3 * N].reshape(N, 3)
+        st = st[st[:, 2] > 0]
+        if not len(st):
+            continue
+        t0 = st[:, 0].min()
+        us = lambda x: np.round(np.asarray(x) / 100.0, 2).tolist()   # noqa: E731  (100 MHz ticks -> us)
+        dur = st[:, 2] - st[:, 0]
+        ends = np.sort(st[:, 2] - t0)
+        res[name + "_span"] = {"waves": int(len(st)), "kernel_us": us(ends[-1]),
+                               "start_spread_us": us(st[:, 0].max() - t0),
+                               "fill_us_mean": us((st[:, 1] - st[:, 0]).mean()),
+                               "wave_us_p0_p50_p90_p99_max": us(np.percentile(dur, [0, 50, 90, 99, 100])),
+                               "end_us_p1_p10_p50_p90_max": us(np.percentile(ends, [1, 10, 50, 90, 100]))}
+elif os.environ.get("HH_DIAG") == "fsm":     # a -DHH_DIAG build: k_cnt phase cycles and walks
     import ctypes as C
     buf = (C.c_uint64 * 16)()
     H.lib().hh_debug_counters(dec._h, buf)
