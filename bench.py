@@ -5,10 +5,11 @@ Workload (BASELINE.json configs[2]): a synthetic 1 GiB English-text .huff --
 kjv.txt tiled (about 349.4 copies) and encoded with the files/kjv.txt.huff
 codebook, cut at a symbol boundary -- decoded on each MI355X.  One "step" is
 one full decode of that stream with the input already resident in HBM:
-hh_decode_device -- the state-machine decode (k_cnt: 128-bit heads, each
+hh_decode_device -- the state-machine decode (k_cntm: 128-bit heads, each
 region's count and exit state in 8-bit steps of the count table, walks
-where a guessed entering state was wrong; k_fscan1/k_fscan2: tile bases;
-k_emf: emission in 7-bit steps into LDS staging, 16-B copy-out) -- plus its
+where a guessed entering state was wrong; k_fscan1: tile bases, its last
+block the block bases; k_emf: emission in 7-bit steps into LDS staging,
+16-B copy-out) -- plus its
 status readback.  For N > 1 the stream is N GiB, sharded
 by whole tiles (weak scaling); each timed step is the rank's segment decode
 (with its prologue tiles), queued asynchronously, no collective inside it --
@@ -516,7 +517,7 @@ def main():
     phases = (phase_split(local, syn.tree, 0, syn.data, syn.bits, out) if world == 1
               else {"sync": None, "scan": None, "emit": None})
     fast = all(s["exact_fallback"] == 0 for s in dev_ms)
-    kernels = ("k_cntm+k_fscan1+k_fscan2+k_emf" if all(s["state_machine"] for s in dev_ms)
+    kernels = ("k_cntm+k_fscan1+k_emf" if all(s["state_machine"] for s in dev_ms)
                else "k_front+k_walk+k_table+k_scan1+k_scan2+k_emit")
     extra = {}
     if world > 1:

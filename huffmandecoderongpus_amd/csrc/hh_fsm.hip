@@ -132,13 +132,15 @@ struct FsmWork {
 // start, max of ~end, max end, sum of (end - start), waves, sum of (fill - start)
 #ifdef HH_WSPAN
 #define WSPAN_N 8192          // wave slots per kernel
-#define WSPAN_START(f) const uint64_t ws_t0_ = __builtin_amdgcn_s_memrealtime(); uint64_t ws_tf_ = ws_t0_; (void)(f)
+#define WSPAN_START(f) const uint64_t ws_t0_ = __builtin_amdgcn_s_memrealtime(); uint64_t ws_tf_ = ws_t0_, ws_ev_ = 0; (void)(f)
+#define WSPAN_EVENT(sh) (ws_ev_ += 1ull << (sh))   // (events per wave in the fill stamp's top bits: walk rounds << 48, fixes << 58)
 #define WSPAN_FILLED() ws_tf_ = __builtin_amdgcn_s_memrealtime()
 #define WSPAN_END(dbg, o) do { const uint64_t t1_ = __builtin_amdgcn_s_memrealtime(); \
     const uint32_t w_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
     if ((threadIdx.x & 63u) == 0 && (dbg) && w_ < WSPAN_N) { uint64_t *d_ = (dbg) + 16 + ((o) ? WSPAN_N * 3 : 0) + 3 * w_; \
-        d_[0] = ws_t0_; d_[1] = ws_tf_; d_[2] = t1_; } } while (0)
+        d_[0] = ws_t0_; d_[1] = ws_tf_ | ws_ev_; d_[2] = t1_; } } while (0)
 #else
+#define WSPAN_EVENT(sh) do {} while (0)
 #define WSPAN_START(f) do {} while (0)
 #define WSPAN_FILLED() do {} while (0)
 #define WSPAN_END(dbg, o) do {} while (0)
@@ -315,13 +317,6 @@ __device__ __forceinline__ uint32_t b1_row(const uint32_t *b1, uint32_t row, uin
     return (v & 255u) << CntFmt<CB>::RS;
 }
 
-// The rare cross-tile fixer out of line: its registers do not add to the
-// count loop's peak (the caller's live values are saved around the call)
-__device__ __noinline__ int cnt_fix_next(const hh_fsm_view *F, const uint32_t *w, uint64_t T1, uint32_t S,
-                                         uint64_t bits, uint32_t x, uint32_t h, uint32_t *fx) {
-    return fsm_fix_next(F, w, T1, S, bits, x, h, fx);
-}
-
 // ---------------------------------------------------------------------------
 // Region passes of k_cnt on words in registers (states as rows).  lim: the
 // region's readable bits (S unless the stream ends inside it); only the TAIL
@@ -426,6 +421,52 @@ __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *
     }
 }
 
+// The rare cross-tile fixer (the chains leaving a tile meet beyond the next
+// tile's region 0): the true chain (state x) and the assumed one (h) walked
+// on through the next tile's regions 1, 2, ... until they meet, at most
+// HH_FSM_KM regions, each region's corrections into f -- fsm_fix_next's rule
+// (hh_fsm_algo.h), run by the whole wave on uniform chains with the region's
+// words in registers, the next region's loaded during the walk.  (Lane 0
+// alone reading every window from global memory: ~25 us per fix, the
+// slowest waves of a 64 MiB count -- per-wave spans of the HH_WSPAN build.)
+// T1: the next tile's first bit (a whole word).  Out of line, by value.
+struct CntFix {
+    uint32_t f[FX_W];
+    uint32_t ok;
+};
+template <uint32_t SW, uint32_t CB>
+__device__ __noinline__ CntFix cnt_fix_wave(const uint32_t *b1, const uint32_t *__restrict__ g, uint64_t nwords, uint64_t bits,
+                                            uint64_t T1, uint32_t x, uint32_t h) {
+    static_assert(FX_W == HH_FSM_KM, "a correction per region a late meeting may be followed into");
+    constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS;
+    CntFix o;
+    for (uint32_t r = 0; r < FX_W; r++) o.f[r] = 0u;
+    uint32_t A = x << RS, B = h << RS, nv[SW], nn[SW];
+    fs_load<SW>(nv, fs_rsrc(g, T1 / 32, nwords), 0);
+    uint32_t r = 0;
+    for (; r < HH_FSM_KM; r++) {
+        const uint64_t R = T1 + (uint64_t)r * S;
+        if (A == B || R >= bits) break;
+        if (r + 1 < HH_FSM_KM) fs_load<SW>(nn, fs_rsrc(g, (R + S) / 32, nwords), 0);   // (the next region's words)
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) asm volatile("" : "+v"(nv[k]));
+        const uint32_t ent = A >> RS;
+        int32_t dd = 0;
+        if (bits - R < S) {
+            walk_region<SW, true, CB>(nullptr, b1, nv, A, B, dd, (uint32_t)(bits - R));
+            if (A != B) dd += (int32_t)(A != 0) - (int32_t)(B != 0);   // (the tail rule)
+        } else {
+            walk_region<SW, false, CB>(nullptr, b1, nv, A, B, dd, S);
+            if (R + S == bits && A != B) dd += (int32_t)(A != 0) - (int32_t)(B != 0);
+        }
+        o.f[r] = fsm_fx(ent, dd);
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) nv[k] = nn[k];
+    }
+    o.ok = r < HH_FSM_KM || A == B ? 1u : 0u;
+    return o;
+}
+
 // ---------------------------------------------------------------------------
 // k_cnt: the count pass of tiles [t0, t1), one tile per wave.  TAIL: the
 // tiles in which the stream ends (or whose next tile's region 0 holds the
@@ -434,6 +475,8 @@ __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *
 __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns, uint32_t cb) {
     return (((ns << (cb + 1)) + ns * 8u + ns) + 15u) & ~15u;
 }
+// The count launches' LDS: the tables, then k_cntm's chunk counter (16 B)
+__host__ __device__ constexpr uint32_t cnt_ctr_off(uint32_t ns, uint32_t cb) { return cnt_tab_bytes(ns, cb); }
 
 // One tile: w = region j's words, nx = region j+1's (lane 63: the next
 // tile's region 0), or (HH_CNT_PNX == 0) loaded here when some lane walks --
@@ -451,6 +494,7 @@ __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns, uint32_t cb) {
 // here from pv, the 16 bytes before the tile).  Returns lane 63's head (the
 // next tile's region-0 guess), as a row.
 #define HIN_NONE 0xffffffffu
+typedef uint32_t __attribute__((address_space(3))) *lds_u32p;
 // decodeallbits: lane j's guess gs for region j+1's entering state (a chain
 // from the root over the last G bits of region j) and (hin == HIN_NONE) lane
 // 0's guess hp for its own region 0: the same head over the previous
@@ -618,13 +662,10 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
             fxv = (j & (FX_W - 1)) == 0 && walked ? fsm_fx(E63, d63) : 0u;
             fsum = walked ? d63 : 0;
         } else {
-            // rare: the chains meet beyond the next tile's region 0 (lane 0,
-            // words from global memory)
-            uint32_t f[FX_W], ok = 1;
+            // rare: the chains meet beyond the next tile's region 0
             const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
-            if (j == 0) ok = cnt_fix_next(&F, g, T0 + TB, S, geo.bits, x, h63, f);
-            else
-                for (int i = 0; i < FX_W; i++) f[i] = 0;
+            const CntFix fo = cnt_fix_wave<SW, CB>(F.b1, g, geo.nwords, geo.bits, T0 + TB, x, h63);
+            const uint32_t *f = fo.f, ok = fo.ok;
 #pragma unroll
             for (int i = 0; i < FX_W; i++) {
                 const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)f[i], 0);
@@ -826,6 +867,12 @@ __host__ __device__ constexpr uint32_t cntm_cw(uint32_t m, uint32_t cb = 8) {
     return m >= 4 ? 10u : cb == 7 ? HH_CNTM7_CW : HH_CNTM2_CW;
 }
 __host__ __device__ constexpr uint32_t cntm_waves(uint32_t m) { return m >= 4 ? 5u : HH_CNTM2_WAVES; }
+#ifndef HH_CNT_CKDIV
+#define HH_CNT_CKDIV 4        // chunks of at most wrun / (waves x CKDIV) tiles, at least 1 (0: wrun / waves)
+#endif
+#ifndef HH_CNT_CHUNK
+#define HH_CNT_CHUNK 4        // k_cntm: count tiles per chunk a wave takes from its workgroup's counter
+#endif
 #ifndef HH_CNT_M
 #define HH_CNT_M 2            // regions per lane of the count pass: 2, 4 (k_cntm) or 1 (k_cnt; HH_CNT_M=n overrides)
 #endif
@@ -898,15 +945,47 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     lds_fill16(smem, tab.ct, ns << (CB + 1));            // (ns x 2^CB u16: a multiple of 16 B)
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
+    // the workgroup's chunk counter, after the tables
+    const uint32_t ctr = cnt_ctr_off(ns, CB);
+    if (tid == 0) *(lds_u32p)(uintptr_t)ctr = 0u;
     __syncthreads();
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts, CB};
     WSPAN_FILLED();
-    // each wave counts a contiguous run of count tiles, in order (lane 0's
-    // entry guess of a tile: the previous tile's lane-63 head)
-    const uint32_t nwv = (gridDim.x - ntb) * CWM, ce = (uint32_t)c1, gw = (blockIdx.x - ntb) * CWM + wv;
-    const uint32_t run = ((uint32_t)(c1 - c0) + nwv - 1) / nwv;
-    uint32_t c = (uint32_t)c0 + gw * run;
-    const uint32_t cend = c + run < ce ? c + run : ce;
+    // Each workgroup counts a contiguous range of count tiles, its waves
+    // taking chunks of ck tiles in turn from the workgroup's LDS counter; a
+    // wave counts a chunk's tiles in order -- lane 0's entry guess of a tile:
+    // the previous tile's lane-63 head; of a chunk's first, a head over the
+    // bytes before it.  (Equal runs per wave: the workgroup's waves ended up
+    // to 50 us apart, per-wave end times of the HH_WSPAN build.  Chunks from
+    // one device-scope counter per XCD instead: count 0.40 -> 0.42 ms.)
+    // ck: HH_CNT_CHUNK tiles, or fewer where a workgroup's range holds fewer
+    // than HH_CNT_CKDIV chunks per wave (small streams: 128 MiB count 0.070
+    // -> 0.063 ms against one chunk per wave)
+    const uint32_t nwg = gridDim.x - ntb, wgi = blockIdx.x - ntb, ce = (uint32_t)c1;
+    const uint32_t wrun = ((uint32_t)(c1 - c0) + nwg - 1) / nwg;
+#if HH_CNT_CKDIV
+    const uint32_t ck = max(1u, min((uint32_t)HH_CNT_CHUNK, wrun / (CWM * HH_CNT_CKDIV)));
+#else
+    const uint32_t ck = min((uint32_t)HH_CNT_CHUNK, (wrun + CWM - 1) / CWM);
+#endif
+    const uint32_t wc0 = (uint32_t)c0 + wgi * wrun < ce ? (uint32_t)c0 + wgi * wrun : ce;
+    const uint32_t wc1 = wc0 + wrun < ce ? wc0 + wrun : ce;
+    const uint32_t nchunk = (wc1 - wc0 + ck - 1) / ck;
+    auto claim = [&]() -> uint32_t {
+        uint32_t u = 0;
+        if (j == 0) u = __hip_atomic_fetch_add((lds_u32p)(uintptr_t)ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return (uint32_t)__builtin_amdgcn_readlane((int)u, 0);
+    };
+    if (c0 == 0 && wgi == 0 && wv == 0) {
+        if (j < FX_W) wk.fx[j] = 0u;                  // (tile 0 has no predecessor to correct it)
+        if (j == 0) wk.fxs[0] = 0;
+    }
+    uint32_t kc = claim();
+    if (kc >= nchunk) {
+        WSPAN_END(wk.dbg, 0);
+        return;
+    }
+    uint32_t c = wc0 + kc * ck, cend = c + ck < wc1 ? c + ck : wc1;
     // region words a region ahead (the next tile's first after a tile's
     // last), the head words (the last region's [HWL, SW)) a tile ahead
     auto load_region = [&](uint32_t *v, uint32_t cc, uint32_t r, uint32_t a, uint32_t b) {
@@ -928,13 +1007,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
                 if (k >= a && k < b) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * (wo + k)), 0, 0);
         }
     };
-    if (c == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
-    if (c == 0 && j == 0) wk.fxs[0] = 0;
-    if (c >= cend) {
-        WSPAN_END(wk.dbg, 0);
-        return;
-    }
-    c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
     // a lane's M regions are adjacent in memory (M * SW words): loaded in one
     // burst, so that every cache line is read once and at once -- loaded a
     // region at a time, the lines of 64 lanes' spans left L1 between their
@@ -944,29 +1016,40 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     uint32_t span[M * SW];
 #pragma unroll
     for (uint32_t r = 0; r < M; r++) load_region(span + r * SW, c, r, 0, SW);
-    // the run's first tile: lane 0's entry guess from the HB bytes before it
-    // (later tiles: the previous tile's lane-63 head) -- once, before the loop
-    uint32_t hin = 0;
-    {
-        uint32_t pv[HB / 4];
-        const uint64_t tw = (uint64_t)c * (64u * M) * SW, pa = tw >= HB / 4 ? tw - HB / 4 : 0u;   // (tile 0: unused)
-        const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (j % (HB / 4))), 0, 0);
-#pragma unroll
-        for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
-        uint32_t gx = 0;
-        if (geo.G) cnt_heads<SW, CB>(smem, span + (M - 1) * SW, pv, geo.G, HIN_NONE, gx, hin);
-        hin = (uint32_t)__builtin_amdgcn_readfirstlane((int)hin);
-    }
+    // the HB bytes before a chunk's first tile (lane i: word i), for lane 0's
+    // entry guess there
+    auto load_pv = [&](uint32_t cc) {
+        const uint64_t tw = (uint64_t)cc * (64u * M) * SW, pa = tw >= HB / 4 ? tw - HB / 4 : 0u;   // (tile 0: unused)
+        uint32_t ln;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        return __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (ln % (HB / 4))), 0, 0);
+    };
+    uint32_t ppv = load_pv(c), hin = HIN_NONE;
     __builtin_amdgcn_s_waitcnt(VMCNT0);
-    for (; c < cend; c++) {
+    for (;;) {
         c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
         const uint64_t Q0 = (uint64_t)c * (64u * M);     // the tile's first region
-        const uint32_t cn = c + 1 < cend ? c + 1 : c;
+        // the next tile: this chunk's next, else the next chunk's first
+        const bool last = c + 1 >= cend;
+        if (last) kc = claim();
+        const bool more = !last || kc < nchunk;
+        const uint32_t cn = !last ? c + 1 : more ? wc0 + kc * ck : c;
         const bool has_next = (uint64_t)(c + 1) * M < geo.ntiles;
         // decodeallbits: lane j's guess for lane j+1's first region, lane 0's
-        // for its own (the previous tile's lane-63 head, or from pv)
-        uint32_t gs = 0, hp = hin;
-        if (geo.G) cnt_heads<SW, CB, false>(smem, span + (M - 1) * SW, nullptr, geo.G, hin, gs, hp);
+        // for its own (the previous tile's lane-63 head, or -- a chunk's first
+        // tile -- a head over the bytes before it, beside lane j's)
+        uint32_t gs = 0, hp = hin == HIN_NONE ? 0u : hin;   // (G = 0: every guess the root)
+        if (geo.G) {
+            if (hin == HIN_NONE) {
+                uint32_t pv[HB / 4];
+#pragma unroll
+                for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
+                cnt_heads<SW, CB>(smem, span + (M - 1) * SW, pv, geo.G, HIN_NONE, gs, hp);
+                hp = (uint32_t)__builtin_amdgcn_readfirstlane((int)hp);
+            } else {
+                cnt_heads<SW, CB, false>(smem, span + (M - 1) * SW, nullptr, geo.G, hin, gs, hp);
+            }
+        }
         const uint32_t gup = shfl_up1(gs);
         const uint32_t sp = j ? gup : (c == 0 ? geo.in_state << RS : hp);
         // the lane's regions in order (records through a buffer resource on
@@ -982,6 +1065,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
             if (r + 1 == M) {
 #pragma unroll
                 for (uint32_t q = 0; q < M; q++) load_region(span + q * SW, cn, q, 0, SW);   // (the next tile's burst)
+                if (last && more) ppv = load_pv(cn);
             }
             uint32_t n;
             const uint32_t X = cnt_region<SW, false, CB>(smem, F.b1, w, s, S, &n);
@@ -997,6 +1081,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         for (int round = 0; round < NR; round++) {
             const bool want = X != E && (j < 63 || has_next);
             if (__ballot(want) == 0) break;
+            WSPAN_EVENT(48);
             // (the tile's records -- and the last round's rewrites -- reached
             // memory: walks read them back)
             __builtin_amdgcn_s_waitcnt(VMCNT0);
@@ -1050,11 +1135,10 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
                 fxv = (j & (FX_W - 1)) == 0 && walked ? fsm_fx(E63, d63) : 0u;
                 fsum = walked ? d63 : 0;
             } else {
-                uint32_t f[FX_W], ok = 1;
                 const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
-                if (j == 0) ok = cnt_fix_next(&F, g, (Q0 + 64u * M) * S, S, geo.bits, x, h63, f);
-                else
-                    for (int i = 0; i < FX_W; i++) f[i] = 0;
+                const CntFix fo = cnt_fix_wave<SW, CB>(F.b1, g, geo.nwords, geo.bits, (Q0 + 64u * M) * S, x, h63);
+                const uint32_t *f = fo.f, ok = fo.ok;
+                WSPAN_EVENT(58);
 #pragma unroll
                 for (int i = 0; i < FX_W; i++) {
                     const uint32_t fv = (uint32_t)__builtin_amdgcn_readlane((int)f[i], 0);
@@ -1074,6 +1158,14 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         // states leaving the emission tiles (the last one's is the tile's)
         wk.xs[(uint64_t)c * M + grp] = (grp == M - 1 ? x : 0u) | fail << 31;
         hin = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
+        if (!more) break;
+        if (last) {
+            c = cn;
+            cend = c + ck < wc1 ? c + ck : wc1;
+            hin = HIN_NONE;
+        } else {
+            c++;
+        }
     }
     WSPAN_END(wk.dbg, 0);
 }
@@ -1252,7 +1344,6 @@ __device__ __forceinline__ u32x4 emf_read16(const uint8_t *lds, uint32_t a) {
 #ifndef HH_EMF_PUT64
 #define HH_EMF_PUT64 1        // k_emf: a step's bytes shifted into the current dword with one 64-bit shift
 #endif
-typedef uint32_t __attribute__((address_space(3))) *lds_u32p;
 template <uint32_t K, bool SWZ = false>
 struct EmfChain {
     uint32_t row, wd, sh, a;
@@ -1753,7 +1844,7 @@ static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sc
     }
 }
 
-static size_t lds_cnt(const FsmDev *fd) { return cnt_tab_bytes(fd->ns, fd->cb); }
+static size_t lds_cnt(const FsmDev *fd) { return cnt_ctr_off(fd->ns, fd->cb) + 16u; }   // (+ k_cntm's chunk counter)
 // k_emf takes the whole LDS (one workgroup per CU) and sizes its stagings
 // from the largest tile output at run time
 #define EMF_LDS (160u * 1024u)

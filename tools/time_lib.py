@@ -84,10 +84,12 @@ if os.environ.get("HH_WSPAN"):             # a -DHH_WSPAN build: per-wave start 
     if os.environ.get("HH_WSPAN_DUMP"):
         np.save(os.environ["HH_WSPAN_DUMP"] + f"_{mib}.npy", a)
     for name, o in (("cnt", 0), ("emf", 3 * N)):
-        st = a[o:o + 3 * N].reshape(N, 3)
+        st = a[o:o + 3 * N].reshape(N, 3).copy()
         st = st[st[:, 2] > 0]
         if not len(st):
             continue
+        ev = st[:, 1] >> 48                    # (events in the fill stamp's top bits: walk rounds, fixes << 10)
+        st[:, 1] &= (1 << 48) - 1
         t0 = st[:, 0].min()
         us = lambda x: np.round(np.asarray(x) / 100.0, 2).tolist()   # noqa: E731  (100 MHz ticks -> us)
         dur = st[:, 2] - st[:, 0]
@@ -97,6 +99,12 @@ if os.environ.get("HH_WSPAN"):             # a -DHH_WSPAN build: per-wave start 
                                "fill_us_mean": us((st[:, 1] - st[:, 0]).mean()),
                                "wave_us_p0_p50_p90_p99_max": us(np.percentile(dur, [0, 50, 90, 99, 100])),
                                "end_us_p1_p10_p50_p90_max": us(np.percentile(ends, [1, 10, 50, 90, 100]))}
+        if ev.any():
+            rounds, fixes = ev & 1023, ev >> 10
+            slow = np.argsort(st[:, 2] - st[:, 0])[-20:]
+            res[name + "_span"].update({"walk_rounds_total": int(rounds.sum()), "walk_rounds_p50_p99_max":
+                                        np.percentile(rounds, [50, 99, 100]).tolist(), "fixes_total": int(fixes.sum()),
+                                        "slowest20_rounds": rounds[slow].tolist(), "slowest20_fixes": fixes[slow].tolist()})
 elif os.environ.get("HH_DIAG") == "fsm":     # a -DHH_DIAG build: k_cnt phase cycles and walks
     import ctypes as C
     buf = (C.c_uint64 * 16)()
