@@ -45,7 +45,7 @@
 #include "hiphuff.h"
 
 #ifdef HH_WSPAN
-#define HH_DBG_WORDS (16 + 6 * 8192)
+#define HH_DBG_WORDS (16 + 10 * 8192)
 #else
 #define HH_DBG_WORDS 16
 #endif

@@ -132,14 +132,19 @@ struct FsmWork {
 // start, max of ~end, max end, sum of (end - start), waves, sum of (fill - start)
 #ifdef HH_WSPAN
 #define WSPAN_N 8192          // wave slots per kernel
-#define WSPAN_START(f) const uint64_t ws_t0_ = __builtin_amdgcn_s_memrealtime(); uint64_t ws_tf_ = ws_t0_, ws_ev_ = 0; (void)(f)
+#define WSPAN_START(f) const uint64_t ws_t0_ = __builtin_amdgcn_s_memrealtime(); uint64_t ws_tf_ = ws_t0_, ws_ev_ = 0, ws_ls_ = 0, ws_ph_[4] = {0, 0, 0, 0}; (void)(f)
+#define WSPAN_MARK() (ws_ls_ = __builtin_amdgcn_s_memrealtime())
+#define WSPAN_PH(i) do { const uint64_t n_ = __builtin_amdgcn_s_memrealtime(); ws_ph_[i] += n_ - ws_ls_; ws_ls_ = n_; } while (0)   // (k_cntm's phases: heads, counts, walks, the rest)
 #define WSPAN_EVENT(sh) (ws_ev_ += 1ull << (sh))   // (events per wave in the fill stamp's top bits: walk rounds << 48, fixes << 58)
 #define WSPAN_FILLED() ws_tf_ = __builtin_amdgcn_s_memrealtime()
 #define WSPAN_END(dbg, o) do { const uint64_t t1_ = __builtin_amdgcn_s_memrealtime(); \
     const uint32_t w_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
     if ((threadIdx.x & 63u) == 0 && (dbg) && w_ < WSPAN_N) { uint64_t *d_ = (dbg) + 16 + ((o) ? WSPAN_N * 3 : 0) + 3 * w_; \
-        d_[0] = ws_t0_; d_[1] = ws_tf_ | ws_ev_; d_[2] = t1_; } } while (0)
+        d_[0] = ws_t0_; d_[1] = ws_tf_ | ws_ev_; d_[2] = t1_; \
+        if (!(o)) for (int i_ = 0; i_ < 4; i_++) (dbg)[16 + 6 * WSPAN_N + 4 * w_ + i_] = ws_ph_[i_]; } } while (0)
 #else
+#define WSPAN_MARK() do {} while (0)
+#define WSPAN_PH(i) do {} while (0)
 #define WSPAN_EVENT(sh) do {} while (0)
 #define WSPAN_START(f) do {} while (0)
 #define WSPAN_FILLED() do {} while (0)
@@ -190,6 +195,7 @@ __device__ __forceinline__ int32_t wave_sum(int32_t v) {
     return v;
 }
 __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1, 64); }
+__device__ __forceinline__ uint32_t shfl_down1(uint32_t v) { return (uint32_t)__shfl_down((int)v, 1, 64); }
 // a wave-uniform 64-bit value in scalar registers (the compiler cannot always
 // tell; a buffer resource built from a vector value costs a waterfall loop)
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
@@ -921,6 +927,60 @@ __device__ __noinline__ CntmWalk cntm_walk(const uint32_t *b1, const uint32_t *_
     return CntmWalk{a, dsum, met ? 1u : 0u};
 }
 
+// HH_WALK_REG: the same walk on the successor's records held in registers
+// (rc: lane j+1's record words, as its count left them or as this lane's
+// earlier rounds rewrote them -- lane j is the only lane that rewrites lane
+// j+1's records), the records stored once after the walks: no record reads,
+// no wait for the tile's stores before a walk.  The successor's words: both
+// regions' loads issued at once.
+template <uint32_t M>
+struct CntmWalkR {
+    uint32_t A;
+    int32_t d;
+    uint32_t met;
+    uint32_t rc[M];
+};
+template <uint32_t SW, uint32_t CB, uint32_t M>
+__device__ __noinline__ CntmWalkR<M> cntm_walk_reg(const uint32_t *b1, const uint32_t *__restrict__ g, uint64_t nwords,
+                                                   uint64_t q0, bool want, uint32_t A, uint32_t B0, CntmWalkR<M> in) {
+    constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS;
+    bool met = !want;
+    uint32_t a = A, b = B0;
+    int32_t dsum = 0;
+    uint32_t nv[M][SW];
+#pragma unroll
+    for (uint32_t r = 0; r < M; r++)
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) nv[r][k] = 0u;
+    if (!met) {
+#pragma unroll
+        for (uint32_t r = 0; r < M; r++) fs_load<SW>(nv[r], fs_rsrc(g, (q0 + r) * SW, nwords), 0);
+    }
+#pragma unroll
+    for (uint32_t r = 0; r < M; r++) {
+        if (__ballot(!met) == 0) break;
+        if (r > 0 && !met) b = fsm_rec_ent(in.rc[r]) << RS;
+#pragma unroll
+        for (uint32_t k = 0; k < SW; k++) asm volatile("" : "+v"(nv[r][k]));
+        uint32_t aa = met ? 0u : a, bb = met ? 0u : b;
+        int32_t dd = 0;
+        walk_region<SW, false, CB>(nullptr, b1, nv[r], aa, bb, dd, S);
+        if (!met) {
+            in.rc[r] = fsm_rec(a >> RS, (uint32_t)((int32_t)fsm_rec_cnt(in.rc[r]) + dd));
+            dsum += dd;
+            met = aa == bb;
+            a = aa;
+        }
+    }
+    in.A = a;
+    in.d = dsum;
+    in.met = met ? 1u : 0u;
+    return in;
+}
+#ifndef HH_WALK_REG
+#define HH_WALK_REG 0         // k_cntm: the walks on records held in registers (above; measured slower: count 0.395 -> 0.42 ms)
+#endif
+
 template <uint32_t SW, uint32_t CB, uint32_t M>
 __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_per_eu(cntm_waves(M), 8))) void k_cntm(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                   uint64_t c0, uint64_t c1, uint64_t u0, uint64_t u1, uint32_t ntb) {
@@ -1028,6 +1088,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     __builtin_amdgcn_s_waitcnt(VMCNT0);
     for (;;) {
         c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+        WSPAN_MARK();
         const uint64_t Q0 = (uint64_t)c * (64u * M);     // the tile's first region
         // the next tile: this chunk's next, else the next chunk's first
         const bool last = c + 1 >= cend;
@@ -1050,6 +1111,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
                 cnt_heads<SW, CB, false>(smem, span + (M - 1) * SW, nullptr, geo.G, hin, gs, hp);
             }
         }
+        WSPAN_PH(0);
         const uint32_t gup = shfl_up1(gs);
         const uint32_t sp = j ? gup : (c == 0 ? geo.in_state << RS : hp);
         // the lane's regions in order (records through a buffer resource on
@@ -1057,6 +1119,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         const __amdgpu_buffer_rsrc_t rrs =
             __builtin_amdgcn_make_buffer_rsrc((void *)(wk.rec + Q0), 0, (int)(64u * M * 4u), 0x00020000);
         uint32_t s = sp, nsum = 0;
+        CntmWalkR<M> wr;
 #pragma unroll
         for (uint32_t r = 0; r < M; r++) {
             uint32_t w[SW];
@@ -1069,11 +1132,20 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
             }
             uint32_t n;
             const uint32_t X = cnt_region<SW, false, CB>(smem, F.b1, w, s, S, &n);
-            __builtin_amdgcn_raw_buffer_store_b32(fsm_rec(s >> RS, n), rrs, (int)(4u * (j * M + r)), 0, 0);
+            if (HH_WALK_REG) wr.rc[r] = fsm_rec(s >> RS, n);   // (lane j's own; lane j-1's view below)
+            else __builtin_amdgcn_raw_buffer_store_b32(fsm_rec(s >> RS, n), rrs, (int)(4u * (j * M + r)), 0, 0);
             nsum += n;
             s = X;
         }
+        WSPAN_PH(1);
         uint32_t X = s, E = gs;
+        uint32_t own[M];                                 // (lane 0 stores its own records)
+#pragma unroll
+        for (uint32_t r = 0; r < M; r++) {
+            own[r] = wr.rc[r];
+            if (HH_WALK_REG) wr.rc[r] = shfl_down1(wr.rc[r]);   // lane j: lane j+1's records
+        }
+
         // makebigtable: walks into the successor's regions (lane 63: into the
         // next tile's region 0, its corrections in fx as in k_cnt)
         int32_t d = 0, dsum = 0;
@@ -1084,14 +1156,21 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
             WSPAN_EVENT(48);
             // (the tile's records -- and the last round's rewrites -- reached
             // memory: walks read them back)
-            __builtin_amdgcn_s_waitcnt(VMCNT0);
+            if (!HH_WALK_REG) __builtin_amdgcn_s_waitcnt(VMCNT0);
             uint32_t A = X;
             bool met;
             if (j < 63) {
-                const CntmWalk cw = cntm_walk<SW, CB, M>(F.b1, g, geo.nwords, wk.rec, Q0 + (uint64_t)(j + 1) * M, want, A, E);
-                A = cw.A;
-                dsum += cw.d;
-                met = cw.met != 0;
+                if (HH_WALK_REG) {
+                    wr = cntm_walk_reg<SW, CB, M>(F.b1, g, geo.nwords, Q0 + (uint64_t)(j + 1) * M, want, A, E, wr);
+                    A = wr.A;
+                    dsum += wr.d;
+                    met = wr.met != 0;
+                } else {
+                    const CntmWalk cw = cntm_walk<SW, CB, M>(F.b1, g, geo.nwords, wk.rec, Q0 + (uint64_t)(j + 1) * M, want, A, E);
+                    A = cw.A;
+                    dsum += cw.d;
+                    met = cw.met != 0;
+                }
             } else {
                 // lane 63: the next tile's region 0 (its own record not written yet)
                 uint32_t nv[SW];
@@ -1115,6 +1194,15 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
             const uint32_t dp = shfl_up1(deep ? 1u : 0u), xa = shfl_up1(A);
             if (j > 0 && dp) X = xa;
         }
+        if (HH_WALK_REG) {
+            // the records: lane j's as lane j-1 left them (lane 0's its own)
+#pragma unroll
+            for (uint32_t r = 0; r < M; r++) {
+                const uint32_t up = shfl_up1(wr.rc[r]);
+                __builtin_amdgcn_raw_buffer_store_b32(j ? up : own[r], rrs, (int)(4u * (j * M + r)), 0, 0);
+            }
+        }
+        WSPAN_PH(2);
         // per emission tile (LG lanes): counts with the walks' corrections
         const uint32_t recv = shfl_up1((uint32_t)dsum);
         int32_t v = (int32_t)nsum + (j ? (int32_t)recv : 0);
@@ -1158,6 +1246,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         // states leaving the emission tiles (the last one's is the tile's)
         wk.xs[(uint64_t)c * M + grp] = (grp == M - 1 ? x : 0u) | fail << 31;
         hin = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
+        WSPAN_PH(3);
         if (!more) break;
         if (last) {
             c = cn;
@@ -2033,7 +2122,7 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
     if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, 16 * sizeof(uint64_t), st));
 #endif
 #if defined(HH_WSPAN)
-    if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, (16 + 6 * WSPAN_N) * sizeof(uint64_t), st));
+    if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, (16 + 10 * WSPAN_N) * sizeof(uint64_t), st));
 #endif
     rc = ws_side(ws);
     if (rc) return rc;

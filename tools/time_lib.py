@@ -78,7 +78,7 @@ if os.environ.get("HH_WSPAN"):             # a -DHH_WSPAN build: per-wave start 
     import ctypes as C
     import numpy as np
     N = 8192
-    buf = (C.c_uint64 * (16 + 6 * N))()
+    buf = (C.c_uint64 * (16 + 10 * N))()
     H.lib().hh_debug_counters(dec._h, buf)
     a = np.ctypeslib.as_array(buf)[16:].astype(np.int64)
     if os.environ.get("HH_WSPAN_DUMP"):
@@ -99,6 +99,10 @@ if os.environ.get("HH_WSPAN"):             # a -DHH_WSPAN build: per-wave start 
                                "fill_us_mean": us((st[:, 1] - st[:, 0]).mean()),
                                "wave_us_p0_p50_p90_p99_max": us(np.percentile(dur, [0, 50, 90, 99, 100])),
                                "end_us_p1_p10_p50_p90_max": us(np.percentile(ends, [1, 10, 50, 90, 100]))}
+        if name == "cnt":                      # (k_cntm's per-wave phase ticks: heads, counts, walks, the rest)
+            ph = a[6 * N:10 * N].reshape(N, 4)[np.nonzero(a[2:3 * N:3] > 0)[0]]
+            tot = ph.sum(axis=1).clip(min=1)
+            res[name + "_span"]["phase_frac_heads_counts_walks_rest"] = np.round(ph.sum(axis=0) / tot.sum(), 4).tolist()
         if ev.any():
             rounds, fixes = ev & 1023, ev >> 10
             slow = np.argsort(st[:, 2] - st[:, 0])[-20:]
