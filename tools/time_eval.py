@@ -24,7 +24,14 @@ if cache and os.path.exists(cache):
 else:
     hf, text = synth.load_source(os.path.join(ROOT, "files"), "kjv.txt")
 syn = synth.tiled_stream(hf, text, mib << 20)
-host = syn.data[: syn.compressed_bytes].cpu().numpy()
+aff = os.environ.get("HH_EVAL_AFFINITY")   # local | remote: the host buffers first touched on the GPU's NUMA node or the other
+cpus = None
+if aff:
+    import bench
+    loc = bench.gpu_local_cpus(0) or set()
+    cpus = loc if aff == "local" else (os.sched_getaffinity(0) - loc)
+    os.sched_setaffinity(0, cpus)
+host = np.array(syn.data[: syn.compressed_bytes].cpu().numpy(), copy=True)
 n = syn.decoded_bytes
 dec = H.Decoder(0, flags=int(os.environ.get("HH_EVAL_FLAGS", "0")))
 dec.set_tree(syn.tree)
@@ -40,7 +47,8 @@ for _ in range(reps):
 res = {"lib": os.path.basename(os.environ.get("HIPHUFF_LIB", H.LIB_PATH)), "mib": mib, "ok": bool(ok),
        "flags": os.environ.get("HH_EVAL_FLAGS", "0"),
        "ms": round(statistics.median(ts) * 1e3, 2), "ms_min": round(min(ts) * 1e3, 2),
-       "all_ms": [round(t * 1e3, 2) for t in ts], "chunk_kb": os.environ.get("HH_PIPE_CHUNK_KB")}
+       "all_ms": [round(t * 1e3, 2) for t in ts], "chunk_kb": os.environ.get("HH_PIPE_CHUNK_KB"),
+       "affinity": aff, "cpus": len(cpus) if cpus else None}
 if os.environ.get("HH_EVAL_DMA"):
     # the PCIe floor: the same byte counts moved by plain async copies
     # between pinned host tensors and the GPU, each way alone and both at once
