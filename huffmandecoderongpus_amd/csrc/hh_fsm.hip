@@ -1933,7 +1933,10 @@ static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sc
     }
 }
 
-static size_t lds_cnt(const FsmDev *fd) { return cnt_ctr_off(fd->ns, fd->cb) + 16u; }   // (+ k_cntm's chunk counter)
+#ifndef HH_XP_CNT_PAD
+#define HH_XP_CNT_PAD 0       // (occupancy experiments: LDS bytes added to the count launches')
+#endif
+static size_t lds_cnt(const FsmDev *fd) { return cnt_ctr_off(fd->ns, fd->cb) + 16u + HH_XP_CNT_PAD; }   // (+ k_cntm's chunk counter)
 // k_emf takes the whole LDS (one workgroup per CU) and sizes its stagings
 // from the largest tile output at run time
 #define EMF_LDS (160u * 1024u)
