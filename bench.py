@@ -337,10 +337,11 @@ def encode_rate(H, hf, text, n: int, dev, reps: int = 5) -> dict:
 
 def copy_rate(dev, nbytes: int, reps: int = 5) -> dict:
     """The HBM rate a plain stream reaches on this GPU, for `frac_vs_copy`
-    (BASELINE.md 3): hh_copy_device -- 16 B per lane loads and stores, 4 in
-    flight per lane, 32 waves per CU -- copying `nbytes` (read + write = 2 x
-    nbytes moved), plain and nontemporal, median of `reps` each; the faster
-    of the two is the reference."""
+    (BASELINE.md 3): hh_copy_device -- one 16-B load and store per lane,
+    n / 256 workgroups of 256 (the fastest shape tools/ubench/ub_copy.hip
+    found) -- copying `nbytes` (read + write = 2 x nbytes moved), plain and
+    nontemporal, median of `reps` each; the faster of the two is the
+    reference."""
     import torch
     import huffmandecoderongpus_amd as H
     nbytes = nbytes // 16 * 16
@@ -357,7 +358,7 @@ def copy_rate(dev, nbytes: int, reps: int = 5) -> dict:
     torch.cuda.empty_cache()
     best = max(res.values())
     return {"GBps": best, "by_policy": res, "bytes_moved": 2 * nbytes,
-            "kernel": "hh_copy_device (16 B/lane, 4 loads in flight per lane)"}
+            "kernel": "hh_copy_device (one 16-B element per lane, n / 256 workgroups of 256, no grid-stride loop)"}
 
 
 def load_pmc(path: str, workload: str):

@@ -2,9 +2,12 @@
 // (frac_vs_copy): how fast a plain HBM stream runs on this GPU, measured on
 // the same box in the same run as the decode.  Not on the decode path.
 //
-// One 16-B load and one 16-B store per lane per element, UNR independent
-// elements in flight per lane, a grid of `wpc` workgroups per CU striding over
-// the buffer; loads and stores with the cache policy given (0 plain, 2 nt).
+// One 16-B load and one 16-B store per lane, one element per lane: a grid of
+// n / 256 workgroups of 256 and no grid-stride loop, loads and stores with
+// the cache policy given (0 plain, 2 nt).  tools/ubench/ub_copy.hip swept the
+// alternatives on 1.5 GB (bench.py's byte count): this shape 6.54 TB/s
+// (read + write) nontemporal; grid-stride loops with 1..8 elements in flight
+// per lane and 2..16 workgroups of 256..1024 per CU 4.7-5.9 TB/s.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -14,24 +17,14 @@
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 #define CP_TB 256
-#define CP_UNR 4
 
 template <int CPOL>
 __global__ __launch_bounds__(CP_TB) void k_copy16(const u32x4 *__restrict__ src, u32x4 *__restrict__ dst, uint64_t n) {
-    const uint64_t step = (uint64_t)gridDim.x * CP_TB * CP_UNR;
-    uint64_t i = (uint64_t)blockIdx.x * CP_TB * CP_UNR + threadIdx.x;
-    for (; i + (CP_UNR - 1) * CP_TB < n; i += step) {
-        u32x4 v[CP_UNR];
-#pragma unroll
-        for (int u = 0; u < CP_UNR; u++)
-            v[u] = CPOL ? __builtin_nontemporal_load(src + i + u * CP_TB) : src[i + u * CP_TB];
-#pragma unroll
-        for (int u = 0; u < CP_UNR; u++) {
-            if (CPOL) __builtin_nontemporal_store(v[u], dst + i + u * CP_TB);
-            else dst[i + u * CP_TB] = v[u];
-        }
-    }
-    for (; i < n; i += CP_TB) dst[i] = src[i];   // (the last partial stride)
+    const uint64_t i = (uint64_t)blockIdx.x * CP_TB + threadIdx.x;
+    if (i >= n) return;
+    const u32x4 v = CPOL ? __builtin_nontemporal_load(src + i) : src[i];
+    if (CPOL) __builtin_nontemporal_store(v, dst + i);
+    else dst[i] = v;
 }
 
 // nbytes: a multiple of 16, both pointers 16-B aligned.  *ms: device time of
@@ -39,14 +32,10 @@ __global__ __launch_bounds__(CP_TB) void k_copy16(const u32x4 *__restrict__ src,
 extern "C" int hh_copy_device(const void *d_src, void *d_dst, uint64_t nbytes, int nt, void *hip_stream, float *ms) {
     if (!d_src || !d_dst || !ms || nbytes % 16 || ((uintptr_t)d_src | (uintptr_t)d_dst) & 15u) return HH_ERR_ARG;
     hipStream_t st = (hipStream_t)hip_stream;
-    int dev = 0, ncu = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return HH_ERR_DEVICE;
     const uint64_t n = nbytes / 16;
-    const uint64_t want = (n + CP_TB * CP_UNR - 1) / (CP_TB * CP_UNR);
-    const uint64_t cap = (uint64_t)ncu * 8;          // 8 workgroups (32 waves) per CU
-    const unsigned grid = (unsigned)(want < cap ? (want ? want : 1) : cap);
+    const uint64_t blocks = (n + CP_TB - 1) / CP_TB;
+    if (blocks > 0x7fffffffull) return HH_ERR_ARG;   // (a grid dimension's limit: 32 TiB)
+    const unsigned grid = (unsigned)(blocks ? blocks : 1);
     hipEvent_t e0, e1;
     if (hipEventCreate(&e0) != hipSuccess) return HH_ERR_DEVICE;
     if (hipEventCreate(&e1) != hipSuccess) { (void)hipEventDestroy(e0); return HH_ERR_DEVICE; }
