@@ -103,7 +103,7 @@ def main():
                                     for k, v in cal.items()}
     with open(os.path.join(out_dir, f"{tag}_kernels.json"), "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
-    if tot_bytes:
+    if tot_bytes and len(sys.argv) <= 2:     # (the headline workload only: bench.py reads it)
         with open(os.path.join(out_dir, "pmc_latest.json"), "w") as f:
             json.dump({"workload": workload, "tag": tag, "hbm_bytes_per_decode": tot_bytes,
                        "per_kernel": {k: d.get("hbm_bytes") for k, d in res["kernels"].items()},

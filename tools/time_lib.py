@@ -3,7 +3,7 @@ the library named by HIPHUFF_LIB (default: the in-tree build); prints one
 JSON line with the median device time of each kernel phase over N runs and
 whether the output matched the tiled text.
 
-    python tools/time_lib.py [MiB] [runs] [source]   (source: kjv.txt | E.coli | bytes)
+    python tools/time_lib.py [MiB] [runs] [source]   (source: kjv.txt | E.coli | bytes | iid)
 """
 import json
 import os
@@ -26,6 +26,10 @@ if src == "bytes":
     # bench's byte-alphabet workload: generated and encoded on the GPU,
     # checked against its symbols (no text to cache)
     hf = text = None
+elif src == "iid":
+    # bench's i.i.d. kjv-unigram workload (symbols checked against the generator)
+    hf0, text0 = synth.load_source(os.path.join(ROOT, "files"), "kjv.txt")
+    hf = text = None
 elif cache and os.path.exists(cache):
     import numpy as np
     hf = H.HuffFile.load(os.path.join(ROOT, "files", src + ".huff"))
@@ -38,6 +42,8 @@ else:
         sys.exit(0)
 if src == "bytes":
     syn = synth.byte_stream(mib << 20)
+elif src == "iid":
+    syn = synth.iid_stream(hf0, text0, mib << 20)
 else:
     syn = synth.tiled_stream(hf, text, mib << 20)
 
