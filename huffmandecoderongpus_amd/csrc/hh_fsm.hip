@@ -85,7 +85,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // per thread before their stores (a loop of 4-B load -> store pairs waited
 // for each load in turn: ~20 round trips to L2 per 42 KB table).  bytes: a
 // multiple of 16; dst and src 16-B aligned.
-template <uint32_t UNR = 4>
+#ifndef HH_FILL_UNR
+#define HH_FILL_UNR 8         // (16-B loads in flight per thread: a 42 or 85 KB table in one round trip)
+#endif
+#ifndef HH_FILL_NT
+#define HH_FILL_NT 1          // (nontemporal loads; plain: 64 MiB emit -1.5 us but 1 GiB +2 % in a same-box A/B)
+#endif
+template <uint32_t UNR = HH_FILL_UNR>
 __device__ __forceinline__ void lds_fill16(uint8_t *dst, const void *src, uint32_t bytes) {
     const u32x4 *s = (const u32x4 *)src;
     u32x4 *d = (u32x4 *)dst;
@@ -94,7 +100,7 @@ __device__ __forceinline__ void lds_fill16(uint8_t *dst, const void *src, uint32
         u32x4 v[UNR];
 #pragma unroll
         for (uint32_t u = 0; u < UNR; u++)
-            if (i + u * step < n) v[u] = __builtin_nontemporal_load(s + i + u * step);
+            if (i + u * step < n) v[u] = HH_FILL_NT ? __builtin_nontemporal_load(s + i + u * step) : s[i + u * step];
 #pragma unroll
         for (uint32_t u = 0; u < UNR; u++)
             if (i + u * step < n) d[i + u * step] = v[u];
