@@ -1273,10 +1273,12 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
 // result slot (k_fscan1's last block; blk / bmax were stored sc1 by every
 // block, so they are read with sc1 loads -- agent-scope atomic loads -- and
 // no cache write-back or invalidate is needed on either side).
-__device__ void fscan_final(const FsmGeo &geo, const FsmWork &wk, uint32_t nblk, uint32_t *res) {
-    __shared__ int64_t s_w[16];
-    __shared__ int32_t s_mx2[16];
-    __shared__ uint32_t s_fl[16];
+// (SC1: the bases and the largest tile output stored sc1, for k_emf's own
+// workgroups to read in the same launch -- HH_SCAN_FUSED; s_w, s_mx2, s_fl:
+// 16 words of LDS each)
+template <bool SC1>
+__device__ __forceinline__ void fscan_final(const FsmGeo &geo, const FsmWork &wk, uint32_t nblk, uint32_t *res, int64_t *s_w,
+                                            int32_t *s_mx2, uint32_t *s_fl) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     int64_t carry = 0;
     int32_t mx = 0;
@@ -1302,7 +1304,10 @@ __device__ void fscan_final(const FsmGeo &geo, const FsmWork &wk, uint32_t nblk,
             base += i < wv ? s_w[i] : 0;
             tot += s_w[i];
         }
-        if (b0 + tid < nblk) wk.blk[b0 + tid] = carry + base + x - v;   // (read by k_emf, after this kernel)
+        if (b0 + tid < nblk) {
+            if (SC1) __hip_atomic_store(&wk.blk[b0 + tid], carry + base + x - v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else wk.blk[b0 + tid] = carry + base + x - v;   // (read by k_emf, after this kernel)
+        }
         carry += tot;
         __syncthreads();
     }
@@ -1322,7 +1327,8 @@ __device__ void fscan_final(const FsmGeo &geo, const FsmWork &wk, uint32_t nblk,
             mx = max(mx, s_mx2[i]);
             fl |= s_fl[i] ? (uint32_t)FF_FAIL : 0u;
         }
-        wk.flags[6] = (uint32_t)mx;       // the largest tile output (symbols)
+        if (SC1) __hip_atomic_store(&wk.flags[6], (uint32_t)mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else wk.flags[6] = (uint32_t)mx;  // the largest tile output (symbols)
         wk.flags[8] = 0u;                 // (the block ticket, for the next decode's k_fscan1)
         const uint32_t lv = geo.ntiles ? wk.xs[geo.ntiles - 1] & 255u : geo.in_state;
         uint32_t en = geo.in_state;
@@ -1348,10 +1354,13 @@ __device__ void fscan_final(const FsmGeo &geo, const FsmWork &wk, uint32_t nblk,
 // (MI355X_MICROARCH.md, the sc1 hand-off table, row 1): each block's totals
 // stored sc1 by one lane, that lane's vmcnt(0), then its agent-scope add to
 // a ticket (flags[8]); the block whose add returns nblk - 1 reads them sc1.
-__global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk, uint32_t nblk, uint32_t *res) {
-    __shared__ int32_t s_tmp[SCAN_TB / 64], s_mx[SCAN_TB / 64];
-    __shared__ uint32_t s_last;
-    const uint64_t t = (uint64_t)blockIdx.x * SCAN_TB + threadIdx.x;
+// Block b's part (SCAN_TB threads); returns (uniform) whether it drew the
+// last ticket.  SC1: the prefixes stored sc1 (HH_SCAN_FUSED).  s_tmp, s_mx:
+// SCAN_TB / 64 words of LDS each, s_last one.
+template <bool SC1>
+__device__ __forceinline__ bool fscan_block(const FsmGeo &geo, const FsmWork &wk, uint32_t b, uint32_t nblk, int32_t *s_tmp,
+                                            int32_t *s_mx, uint32_t *s_last) {
+    const uint64_t t = (uint64_t)b * SCAN_TB + threadIdx.x;
     int32_t c = 0;
     if (t < geo.ntiles && t >= geo.emit_from) c = wk.tsum[t] + wk.fxs[t];
     // a tile whose last chain met no other within HH_FSM_KM regions (k_cnt
@@ -1373,16 +1382,32 @@ __global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk, uint
         tot += v;
         mx = max(mx & ~BMAX_FAIL, s_mx[i] & ~BMAX_FAIL) | ((mx | s_mx[i]) & BMAX_FAIL);
     }
-    if (t <= geo.ntiles) wk.lex[t] = base + x - c;
-    if (threadIdx.x == 0) {
-        __hip_atomic_store(&wk.blk[blockIdx.x], (int64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&wk.bmax[blockIdx.x], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t <= geo.ntiles) {
+        if (SC1) __hip_atomic_store(&wk.lex[t], base + x - c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else wk.lex[t] = base + x - c;
+    }
+    if (SC1) {
+        // (every thread's prefix stored before the block's ticket: k_emf's
+        // workgroups read them in this launch)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        s_last = __hip_atomic_fetch_add(&wk.flags[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1u;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(&wk.blk[b], (int64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&wk.bmax[b], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (SC1: this thread's stores only -- see k_emf)
+        *s_last = __hip_atomic_fetch_add(&wk.flags[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1u;
     }
     __syncthreads();
-    if (!s_last) return;
-    fscan_final(geo, wk, nblk, res);
+    return *s_last != 0;
+}
+__global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk, uint32_t nblk, uint32_t *res) {
+    __shared__ int32_t s_tmp[SCAN_TB / 64], s_mx[SCAN_TB / 64];
+    __shared__ uint32_t s_last;
+    __shared__ int64_t s_w[16];
+    __shared__ int32_t s_mx2[16];
+    __shared__ uint32_t s_fl[16];
+    if (fscan_block<false>(geo, wk, blockIdx.x, nblk, s_tmp, s_mx, &s_last)) fscan_final<false>(geo, wk, nblk, res, s_w, s_mx2, s_fl);
 }
 
 // ---------------------------------------------------------------------------
@@ -1491,6 +1516,9 @@ struct EmfChain {
 };
 #ifndef HH_EMF_PIPE
 #define HH_EMF_PIPE 1         // k_emf: step k+1's table read issued before step k's symbols are stored
+#endif
+#ifndef HH_SCAN_FUSED
+#define HH_SCAN_FUSED 0       // the tile scan inside the emission launch (k_emf), not a launch of its own
 #endif
 #ifndef HH_EMF_DYN
 #define HH_EMF_DYN 1          // k_emf: the workgroup's tiles claimed one at a time from an LDS counter
@@ -1652,7 +1680,7 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
 template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO, bool SWZ>
 __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const FsmGeo &geo, const FsmTab &tab,
                                         const FsmWork &wk, uint8_t *__restrict__ out, uint64_t cap, uint64_t t0,
-                                        uint64_t t1, uint32_t lds_bytes, uint32_t blk, uint32_t nblk) {
+                                        uint64_t t1, uint32_t lds_bytes, uint32_t blk, uint32_t nblk, uint32_t epoch) {
     static_assert(!TAIL || NCH == 1, "the tail tiles take one chain per lane");
     static_assert(!SWZ || !TAIL, "the tail tiles' staging is not swizzled");
     extern __shared__ __align__(16) uint8_t smem[];
@@ -1672,7 +1700,16 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     constexpr bool DYN = !TAIL && NCH == 1 && HH_EMF_DYN;
     const uint32_t ctr = lds_bytes - 16u;
     if (DYN && tid == 0) *(lds_u32p)(uintptr_t)ctr = 0u;
+    if (epoch && tid == 0) {
+        // HH_SCAN_FUSED: the scan's last block (k_emf's own workgroups, above)
+        // has published the bases (stored sc1)
+        while (__hip_atomic_load(&wk.flags[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) __builtin_amdgcn_s_sleep(1);
+    }
     __syncthreads();
+    // (then this CU's and XCD's caches invalidated, once: the bases, prefixes
+    // and the largest tile output are read with plain loads -- sc1 loads in
+    // the tile loop cost the emission 3 %)
+    if (epoch) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // staging per tile: the largest tile output + its 16-B misalignment + the
     // last step's overflow dword; the active waves share the rest of the LDS
     const uint32_t tabb = SWZ ? (emf_tab_bytes(ns, K, r) + 127u) & ~127u : emf_tab_bytes(ns, K, r);   // (SWZ: 128-B chunks)
@@ -1873,15 +1910,49 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
 // first, resident beside the rest) emit the stream's last tiles [u0, u1)
 // with the stream-end checks (TAIL) -- a launch of their own after this one
 // cost a tile's time at the end of every decode.
+// HH_SCAN_FUSED (epoch != 0): the tile scan runs here, not in k_fscan1 --
+// the launch's workgroups claim its sblk blocks one at a time from a counter
+// (flags[11], never reset: every workgroup claims until a claim fails, so a
+// decode takes sblk + gridDim.x counts and the host passes this decode's
+// first, cbase), so that only workgroups already running do scan work and
+// none waits on one that has not started; the block that draws the last
+// ticket scans the block totals and publishes the bases sc1 with flags[10]
+// = epoch; then every workgroup fills its tables and waits for the flag.
+// The launch and the drain of k_fscan1 are gone.  (A compare-and-swap
+// counter tagged with the epoch instead: 257 workgroups contending for it
+// took 0.4 ms.)
 template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO, bool SWZ = false>
 __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1,
-                                                 uint32_t lds_bytes, uint64_t u0, uint64_t u1, uint32_t ntb) {
+                                                 uint32_t lds_bytes, uint64_t u0, uint64_t u1, uint32_t ntb, uint32_t sblk,
+                                                 uint32_t epoch, uint32_t cbase, uint32_t *res) {
+    if (epoch) {
+        static_assert(64 * emf_waves(NCH) == SCAN_TB || NCH != 1, "a scan block per workgroup");
+        extern __shared__ __align__(16) uint8_t smem[];
+        int32_t *s_tmp = (int32_t *)smem, *s_mx = s_tmp + 16, *s_mx2 = s_tmp + 32;
+        uint32_t *s_last = (uint32_t *)(s_tmp + 48), *s_fl = (uint32_t *)(s_tmp + 64);
+        uint32_t *s_b = (uint32_t *)(s_tmp + 80);
+        int64_t *s_w = (int64_t *)(smem + 512);
+        for (;;) {
+            if (threadIdx.x == 0) *s_b = __hip_atomic_fetch_add(&wk.flags[11], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - cbase;
+            __syncthreads();
+            const uint32_t b = *s_b;
+            __syncthreads();
+            if (b >= sblk) break;
+            if (fscan_block<true>(geo, wk, b, sblk, s_tmp, s_mx, s_last)) {
+                fscan_final<true>(geo, wk, sblk, res, s_w, s_mx2, s_fl);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0) __hip_atomic_store(&wk.flags[10], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+        }
+    }
     if (!TAIL && blockIdx.x < ntb) {
-        emf_run<SW, K, true, 1, false, false>(g, geo, tab, wk, out, cap, u0, u1, lds_bytes, blockIdx.x, ntb);
+        emf_run<SW, K, true, 1, false, false>(g, geo, tab, wk, out, cap, u0, u1, lds_bytes, blockIdx.x, ntb, epoch);
         return;
     }
-    emf_run<SW, K, TAIL, NCH, SCO, SWZ>(g, geo, tab, wk, out, cap, t0, t1, lds_bytes, blockIdx.x - ntb, gridDim.x - ntb);
+    emf_run<SW, K, TAIL, NCH, SCO, SWZ>(g, geo, tab, wk, out, cap, t0, t1, lds_bytes, blockIdx.x - ntb, gridDim.x - ntb, epoch);
 }
 
 // ---------------------------------------------------------------------------
@@ -1890,7 +1961,7 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
 typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint64_t);
 typedef void (*kcntm_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t);
 typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t, uint32_t, uint64_t,
-                       uint64_t, uint32_t);
+                       uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t *);
 
 #define FSM_SW_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
 // k_cntm for regions of S = 32 sw bits with count steps of cb bits (M =
@@ -2061,7 +2132,8 @@ static int ws_need(FsmWs *ws, size_t need) {
     const size_t sz = need + need / 8;
     if (hipMalloc(&ws->p, sz) != hipSuccess) return HH_ERR_NOMEM;
     ws->size = sz;
-    FS_OK(hipMemset(ws->p, 0, 64));   // the status word and the scan's block ticket; k_fscan1's last block clears them
+    FS_OK(hipMemset(ws->p, 0, 64));   // the status word and the scan's block ticket (the scan's last block clears it)
+    ws->cbase = 0;                     // (the fused scan's block counter, flags[11], starts again)
     return HH_OK;
 }
 
@@ -2173,15 +2245,24 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
         }
     }
     if (fd->phases) FS_OK(hipEventRecord(ev[1], st));
-    hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk, nblk, ws->d_res + 16 * slot);
-    FS_OK(hipGetLastError());
+    // tiles that end before the stream, then the last one(s) (TAIL: the main
+    // emission launch's first workgroups; a launch of their own without
+    // tiles before them)
+    const uint64_t ne = std::max<uint64_t>(emit_from, std::min<uint64_t>(bits / TB, nt));
+    // the scan inside the main emission launch (HH_SCAN_FUSED), else k_fscan1
+    const bool fused = HH_SCAN_FUSED && emit_from < nt && ne > emit_from && emf_nch() == 1 && nblk < 0xf000u &&
+                       !getenv("HH_NO_SCAN_FUSED");
+    uint32_t epoch = 0;
+    if (fused) {
+        if (++ws->epoch == 0) ws->epoch = 1;
+        epoch = ws->epoch;
+    } else {
+        hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk, nblk, ws->d_res + 16 * slot);
+        FS_OK(hipGetLastError());
+    }
     if (fd->phases) FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
         const uint32_t ew = emf_waves(emf_nch()), ew1 = emf_waves(1);
-        // tiles that end before the stream, then the last one(s) (TAIL: the
-        // main launch's first workgroups; a launch of its own without tiles
-        // before them)
-        const uint64_t ne = std::max<uint64_t>(emit_from, std::min<uint64_t>(bits / TB, nt));
         const uint32_t ntb = (uint32_t)((nt - ne + ew1 - 1) / ew1);
         if (ne > emit_from) {
             const uint64_t nwg = (ne - emit_from + ew - 1) / ew;
@@ -2191,12 +2272,13 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
             if (HH_XP_EMF && getenv("HH_EMF_POOL")) ldsb = emf_tab_bytes(fd->ns, fd->K, fd->r) + (uint32_t)atoi(getenv("HH_EMF_POOL"));
             hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch(), fd->sco, fd->swz), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne,
-                               ldsb, ne, nt, ntb);
+                               ldsb, ne, nt, ntb, fused ? nblk : 0u, epoch, ws->cbase, ws->d_res + 16 * slot);
             FS_OK(hipGetLastError());
+            if (fused) ws->cbase += nblk + ge;   // (the counts this launch takes: see k_emf)
         } else if (ne < nt) {
             hipLaunchKernelGGL(kemf_for(sw, fd->K, true, 1, false), dim3(ntb), dim3(64 * ew1), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt,
-                               (uint32_t)lds_emf(fd), (uint64_t)0, (uint64_t)0, 0u);
+                               (uint32_t)lds_emf(fd), (uint64_t)0, (uint64_t)0, 0u, 0u, 0u, 0u, (uint32_t *)nullptr);
             FS_OK(hipGetLastError());
         }
     }

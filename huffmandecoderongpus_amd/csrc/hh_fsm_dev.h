@@ -48,6 +48,8 @@ struct FsmWs {
     // decode.  FSM_RES_SLOTS slots of 16 words: a decode in flight and the
     // next one enqueued behind it (hh_decode_device_async) keep theirs apart.
     uint32_t *h_res, *d_res;
+    uint32_t epoch;           // the last decode's tag for the scan inside k_emf (HH_SCAN_FUSED)
+    uint32_t cbase;           // that scan's block counter (flags[11]) at the next decode's start
 };
 #define FSM_RES_SLOTS 2
 // What fsm_collect needs of a decode fsm_launch enqueued.
