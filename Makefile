@@ -40,7 +40,11 @@ $(BUILD)/hh_device.o: $(CSRC)/hh_device.hip $(CSRC)/hh_algo.h $(CSRC)/hh_interna
                       $(CSRC)/hh_fsm.h $(CSRC)/hh_fsm_algo.h include/hiphuff.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(BUILD)/hh_fsm.o: $(CSRC)/hh_fsm.hip $(CSRC)/hh_fsm_dev.h $(CSRC)/hh_fsm.h $(CSRC)/hh_fsm_algo.h \
+$(BUILD)/hh_one.o: $(CSRC)/hh_one.hip $(CSRC)/hh_fsm_kern.h $(CSRC)/hh_fsm_dev.h $(CSRC)/hh_fsm.h $(CSRC)/hh_fsm_algo.h \
+                   $(CSRC)/hh_internal.h include/hiphuff.h | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/hh_fsm.o: $(CSRC)/hh_fsm.hip $(CSRC)/hh_fsm_kern.h $(CSRC)/hh_fsm_dev.h $(CSRC)/hh_fsm.h $(CSRC)/hh_fsm_algo.h \
                    $(CSRC)/hh_internal.h include/hiphuff.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -50,7 +54,7 @@ $(BUILD)/hh_encode.o: $(CSRC)/hh_encode.hip $(CSRC)/hh_internal.h include/hiphuf
 $(BUILD)/hh_probe.o: $(CSRC)/hh_probe.hip include/hiphuff.h | $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(BUILD)/hh_device.o $(BUILD)/hh_fsm.o $(BUILD)/hh_encode.o $(BUILD)/hh_probe.o $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
+$(LIB): $(BUILD)/hh_device.o $(BUILD)/hh_fsm.o $(BUILD)/hh_one.o $(BUILD)/hh_encode.o $(BUILD)/hh_probe.o $(BUILD)/hh_huff.o $(BUILD)/hh_plugin.o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $@ $^
 
 $(CLI): $(PKG)/host/hh_cli.c $(LIB) include/hiphuff.h include/hiphuff_plugin.h
@@ -80,7 +84,8 @@ clean:
 variant: $(BUILD)/hh_plugin.o $(BUILD)/hh_encode.o $(BUILD)/hh_probe.o
 	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/hh_device.hip -o $(BUILD)/hh_device_$(V).o
 	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/hh_fsm.hip -o $(BUILD)/hh_fsm_$(V).o
+	$(HIPCC) $(HIPFLAGS) -c $(CSRC)/hh_one.hip -o $(BUILD)/hh_one_$(V).o
 	$(CC) $(CFLAGS) $(HIPEXTRA) -c $(CSRC)/hh_huff.c -o $(BUILD)/hh_huff_$(V).o
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -o $(BUILD)/libhiphuff_$(V).so $(BUILD)/hh_device_$(V).o \
-	    $(BUILD)/hh_fsm_$(V).o $(BUILD)/hh_huff_$(V).o $(BUILD)/hh_encode.o $^
+	    $(BUILD)/hh_fsm_$(V).o $(BUILD)/hh_one_$(V).o $(BUILD)/hh_huff_$(V).o $^
 .PHONY: variant

@@ -83,6 +83,7 @@ FLAG_NO_FIXED = 4     # HH_FLAG_NO_FIXED: fixed-length codes through the general
 FLAG_LEGACY = 8       # HH_FLAG_LEGACY: round 2's pipeline instead of the state-machine decode
 FLAG_PHASE_TIMING = 16  # HH_FLAG_PHASE_TIMING: events between the kernels (ms_sync/scan/emit)
 FLAG_KEEP_HOST_PINNED = 32  # HH_FLAG_KEEP_HOST_PINNED: decode_host keeps the caller's buffers page-locked
+FLAG_TWO_PASS = 64    # HH_FLAG_TWO_PASS: the state machine's two-pass form instead of its single pass
 _lib_handle: Optional[C.CDLL] = None
 
 # exported symbols and their ctypes signatures; tests check every one of these

@@ -1651,7 +1651,13 @@ extern "C" int hh_decoder_set_tree(hh_decoder *d, const hh_tree *tree) {
         const int urc = fsm_upload(&d->fsm, d->ft, Gf, (uint32_t)d->ht->minlen, (uint32_t)d->ht->maxlen);
         d->fsm.dbg = d->d_dbg;
         d->fsm.phases = (d->cfg.flags & HH_FLAG_PHASE_TIMING) != 0;
+        d->fsm.two_pass = (d->cfg.flags & HH_FLAG_TWO_PASS) != 0;
         if (urc != HH_OK && urc != HH_ERR_UNSUPPORTED) return urc;
+        // the single pass (hh_one.hip): its head over the emission table's
+        // K-bit steps, on the code lattice like the count pass's
+        uint32_t G1 = hh_fsm_pick_head(d->ht, d->S, d->ft->K);
+        if (getenv("HH_FSM_HEAD")) G1 = (uint32_t)atoi(getenv("HH_FSM_HEAD")) / d->ft->K * d->ft->K;   // experiments
+        if (urc == HH_OK) one_setup(&d->fsm, G1 > d->S ? 0u : G1, avg, (uint32_t)d->ht->minlen);
     }
     d->have_tree = 1;
     return HH_OK;
@@ -2045,14 +2051,14 @@ static bool fsm_path_ok(const hh_decoder *d) {
     return d->fsm.ok && !(d->cfg.flags & (HH_FLAG_LEGACY | HH_FLAG_FORCE_EXACT | HH_FLAG_FORCE_SEGMENT));
 }
 // ms: count, scan, emission (HH_FLAG_PHASE_TIMING; else 0), total
-static void fsm_stats(hh_decoder *d, uint64_t bits, uint64_t total, const float *ms) {
+static void fsm_stats(hh_decoder *d, uint64_t bits, uint64_t total, const float *ms, uint32_t one) {
     d->stats.ms_sync = ms[0];
     d->stats.ms_scan = ms[1];
     d->stats.ms_emit = ms[2];
     d->stats.ms_total = ms[3];
     d->stats.lanes = (bits + d->S - 1) / d->S;
     d->stats.out_len = total;
-    d->stats.state_machine = 1;
+    d->stats.state_machine = one ? 2 : 1;
 }
 
 extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits, void *d_out,
@@ -2077,7 +2083,7 @@ extern "C" int hh_decode_device(hh_decoder *d, const void *d_data, uint64_t bits
         float ms[4] = {0, 0, 0, 0};
         const int rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, d_data, bits, 0, 0, 0, d_out, cap, st,
                                   &total, &leave, &en, ms);
-        fsm_stats(d, bits, total, ms);
+        fsm_stats(d, bits, total, ms, d->fsm_ws.last_one);
         if (rc == HH_NOSYNC) {
             // chains that did not meet within HH_FSM_KM regions: a code that
             // does not resynchronise
@@ -2144,7 +2150,19 @@ static int async_check(hh_decoder *d) {
         uint32_t leave = 0, en = 0;
         float ms[4] = {0, 0, 0, 0};
         rc = fsm_collect(&d->fsm_ws, ev, &d->apend.pd, &total, &leave, &en, ms);
-        fsm_stats(d, d->apend.bits, total, ms);
+        uint32_t one = d->apend.pd.one;
+        if (rc == HH_ONE_RETRY) {
+            // the single pass handed the decode back: the two passes decode
+            // it again, synchronously, on the decode's stream
+            FsmPend p2;
+            memset(&p2, 0, sizeof(p2));
+            rc = fsm_launch(&d->fsm, &d->fsm_ws, d->apend.pd.slot, ev, d->apend.d_data, d->apend.bits,
+                            d->apend.pd.nt_arg, d->apend.pd.in_state, d->apend.pd.emit_from, d->apend.d_out,
+                            d->apend.pd.cap, d->apend.st, &p2, true);
+            if (rc == HH_OK) rc = fsm_collect(&d->fsm_ws, ev, &p2, &total, &leave, &en, ms);
+            one = 0;
+        }
+        fsm_stats(d, d->apend.bits, total, ms, one);
         *d->apend.out_len = total;
         if (d->apend.ro) {
             // a segment: its states; one that does not resynchronise is
@@ -2258,7 +2276,7 @@ extern "C" int hh_decode_device_range(hh_decoder *d, const void *d_data, const h
         const int rc = fsm_decode(&d->fsm, &d->fsm_ws, d->h_flags, d->ev, d_data, rg->bits_avail, rg->ntiles,
                                   rg->in_state, rg->prologue, d_out, cap, st, &ro->out_len, &ro->leave_state,
                                   &ro->entry_state, ms);
-        fsm_stats(d, rg->bits_avail, ro->out_len, ms);
+        fsm_stats(d, rg->bits_avail, ro->out_len, ms, d->fsm_ws.last_one);
         if (rc == HH_NOSYNC) return HH_ERR_UNSUPPORTED;   // (decode such a code whole)
         // the state leaving a segment does not depend on how it was entered
         // once the chain from its entry has met an entry-independent one
@@ -2519,7 +2537,7 @@ static int host_pipeline(hh_decoder *d, const uint8_t *data, uint64_t bits, uint
         (void)hipHostUnregister((void *)data);
         if (cap) (void)hipHostUnregister(out);
     }
-    fsm_stats(d, bits, total, ms_all);
+    fsm_stats(d, bits, total, ms_all, d->fsm_ws.last_one);
     *out_len = total;
     return rc == HH_NOSYNC ? HH_ERR_UNSUPPORTED : rc;   // (no resync: the serial path decodes it whole)
 }

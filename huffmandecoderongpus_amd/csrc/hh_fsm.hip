@@ -32,81 +32,15 @@
 #include <algorithm>
 #include <type_traits>
 
-#include "hh_fsm_algo.h"
-#include "hh_fsm_dev.h"
-#include "hiphuff.h"
+#include "hh_fsm_kern.h"
 
-#define FS_OK(x)                                                              \
-    do {                                                                      \
-        hipError_t e_ = (x);                                                  \
-        if (e_ != hipSuccess) {                                               \
-            fprintf(stderr, "hiphuff: %s failed: %s\n", #x, hipGetErrorString(e_)); \
-            return HH_ERR_DEVICE;                                             \
-        }                                                                     \
-    } while (0)
-
-#define NR 64                 // regions per tile (a wave)
-#ifndef HH_CW
-#define HH_CW 16
-#endif
-#define CW HH_CW               // k_cnt: waves per workgroup
-#ifndef HH_CNT_PNX
-#define HH_CNT_PNX 0          // k_cnt walks: region j+1's words prefetched a tile ahead (1) or loaded at
-                              // a walk (0); reading them from lane j+1 measured no faster
-#endif
-#ifndef HH_CNT_IL
-#define HH_CNT_IL 0           // k_cnt: the next tile's heads interleaved with this tile's counts (measured no faster)
-#endif
-#ifndef HH_CNT_DADD
-#define HH_CNT_DADD 1         // k_cnt(m): a count step's entry added after the next step's read is issued
-#endif
-#ifndef HH_WALK_MASK
-#define HH_WALK_MASK 1        // k_cnt walks: only the lanes not met yet look up
-#endif
-#ifndef HH_WALK_CHK
-#define HH_WALK_CHK 1         // k_cnt walks: ask whether every lane has met every HH_WALK_CHK + 1 steps
-#endif
-// k_emf: waves per workgroup (at most; the active ones are sized at run time)
-// for NCH chains per lane -- two chains need the register room of 12 waves
-#ifndef HH_EMF2_WAVES
-#define HH_EMF2_WAVES 12
-#endif
-__host__ __device__ constexpr uint32_t emf_waves(uint32_t nch) { return nch == 2 ? HH_EMF2_WAVES : 16u; }
+#define CW 16                 // k_cnt: waves per workgroup
+__host__ __device__ constexpr uint32_t emf_waves() { return 16u; }   // k_emf: waves per workgroup (at most)
 #define SCAN_TB 1024          // tiles per k_fscan1 block
 #define FX_W 8                // corrections per tile (HH_FSM_KM)
-#define VMCNT0 0x0F70         // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15): vector memory only
 static_assert(FX_W == HH_FSM_KM, "corrections per tile");
 
 enum { FF_FAIL = 1, FF_OVER = 2 };
-
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-// A table into LDS at a workgroup's start: 16-B loads, UNR of them in flight
-// per thread before their stores (a loop of 4-B load -> store pairs waited
-// for each load in turn: ~20 round trips to L2 per 42 KB table).  bytes: a
-// multiple of 16; dst and src 16-B aligned.
-#ifndef HH_FILL_UNR
-#define HH_FILL_UNR 8         // (16-B loads in flight per thread: a 42 or 85 KB table in one round trip)
-#endif
-#ifndef HH_FILL_NT
-#define HH_FILL_NT 1          // (nontemporal loads; plain: 64 MiB emit -1.5 us but 1 GiB +2 % in a same-box A/B)
-#endif
-template <uint32_t UNR = HH_FILL_UNR>
-__device__ __forceinline__ void lds_fill16(uint8_t *dst, const void *src, uint32_t bytes) {
-    const u32x4 *s = (const u32x4 *)src;
-    u32x4 *d = (u32x4 *)dst;
-    const uint32_t n = bytes / 16u, step = blockDim.x;
-    for (uint32_t i = threadIdx.x; i < n; i += UNR * step) {
-        u32x4 v[UNR];
-#pragma unroll
-        for (uint32_t u = 0; u < UNR; u++)
-            if (i + u * step < n) v[u] = HH_FILL_NT ? __builtin_nontemporal_load(s + i + u * step) : s[i + u * step];
-#pragma unroll
-        for (uint32_t u = 0; u < UNR; u++)
-            if (i + u * step < n) d[i + u * step] = v[u];
-    }
-}
-typedef uint32_t u32u __attribute__((aligned(1)));   // an LDS word at any byte address
 
 struct FsmGeo {
     uint64_t bits;        // stream length of the segment
@@ -128,170 +62,7 @@ struct FsmWork {
     int32_t *lex;         // [ntiles + 1] exclusive prefix within the scan block
     int64_t *blk;         // [nblk] block totals, then block bases
     int32_t *bmax;        // [nblk] the block's largest tile count (k_emf sizes its staging by it)
-    uint64_t *dbg;        // HH_DIAG builds: [0..3] k_cnt phase cycles (head, count, walks, records),
-                          // [8] tiles, [9] tiles with a walk, [10] walk rounds
 };
-
-// HH_WSPAN builds: when the waves of k_cntm (dbg[0..6]) and k_emf
-// (dbg[8..14]) start, finish their table fill and end, on the global
-// 100 MHz clock (s_memrealtime): max of ~start (-> earliest start), max
-// start, max of ~end, max end, sum of (end - start), waves, sum of (fill - start)
-#ifdef HH_WSPAN
-#define WSPAN_N 8192          // wave slots per kernel
-#define WSPAN_START(f) const uint64_t ws_t0_ = __builtin_amdgcn_s_memrealtime(); uint64_t ws_tf_ = ws_t0_, ws_ev_ = 0, ws_ls_ = 0, ws_ph_[4] = {0, 0, 0, 0}; (void)(f)
-#define WSPAN_MARK() (ws_ls_ = __builtin_amdgcn_s_memrealtime())
-#define WSPAN_PH(i) do { const uint64_t n_ = __builtin_amdgcn_s_memrealtime(); ws_ph_[i] += n_ - ws_ls_; ws_ls_ = n_; } while (0)   // (k_cntm's phases: heads, counts, walks, the rest)
-#define WSPAN_EVENT(sh) (ws_ev_ += 1ull << (sh))   // (events per wave in the fill stamp's top bits: walk rounds << 48, fixes << 58)
-#define WSPAN_FILLED() ws_tf_ = __builtin_amdgcn_s_memrealtime()
-#define WSPAN_END(dbg, o) do { const uint64_t t1_ = __builtin_amdgcn_s_memrealtime(); \
-    const uint32_t w_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); \
-    if ((threadIdx.x & 63u) == 0 && (dbg) && w_ < WSPAN_N) { uint64_t *d_ = (dbg) + 16 + ((o) ? WSPAN_N * 3 : 0) + 3 * w_; \
-        d_[0] = ws_t0_; d_[1] = ws_tf_ | ws_ev_; d_[2] = t1_; \
-        if (!(o)) for (int i_ = 0; i_ < 4; i_++) (dbg)[16 + 6 * WSPAN_N + 4 * w_ + i_] = ws_ph_[i_]; } } while (0)
-#else
-#define WSPAN_MARK() do {} while (0)
-#define WSPAN_PH(i) do {} while (0)
-#define WSPAN_EVENT(sh) do {} while (0)
-#define WSPAN_START(f) do {} while (0)
-#define WSPAN_FILLED() do {} while (0)
-#define WSPAN_END(dbg, o) do {} while (0)
-#endif
-#ifdef HH_DIAG
-#define CDIAG_DECL uint64_t cg_acc[4] = {0, 0, 0, 0}, cg_n[3] = {0, 0, 0}; uint64_t cg_t = __builtin_amdgcn_s_memtime();
-#define CDIAG_STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); cg_acc[i] += t_ - cg_t; cg_t = t_; } while (0)
-#define CDIAG_COUNT(i, v) do { cg_n[i] += (v); } while (0)
-#define CDIAG_FLUSH(dbg) do { if ((threadIdx.x & 63u) == 0) { for (int i_ = 0; i_ < 4; i_++) atomicAdd((unsigned long long *)&(dbg)[i_], (unsigned long long)cg_acc[i_]); \
-    for (int i_ = 0; i_ < 3; i_++) atomicAdd((unsigned long long *)&(dbg)[8 + i_], (unsigned long long)cg_n[i_]); } } while (0)
-#define EDIAG_DECL uint64_t eg_acc[4] = {0, 0, 0, 0}; uint64_t eg_t = __builtin_amdgcn_s_memtime();
-#define EDIAG_STAMP(i) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); eg_acc[i] += t_ - eg_t; eg_t = t_; } while (0)
-#define EDIAG_FLUSH(dbg) do { if ((threadIdx.x & 63u) == 0) for (int i_ = 0; i_ < 4; i_++) atomicAdd((unsigned long long *)&(dbg)[4 + i_], (unsigned long long)eg_acc[i_]); } while (0)
-#else
-#define EDIAG_DECL
-#define EDIAG_STAMP(i) do {} while (0)
-#define EDIAG_FLUSH(dbg) do {} while (0)
-#define CDIAG_DECL
-#define CDIAG_STAMP(i) do {} while (0)
-#define CDIAG_COUNT(i, v) do {} while (0)
-#define CDIAG_FLUSH(dbg) do {} while (0)
-#endif
-
-struct FsmTab {
-    const uint16_t *ct;
-    const uint32_t *b1;
-    const uint8_t *tsym;
-    const uint64_t *et;
-    const uint64_t *er;
-};
-
-// ---------------------------------------------------------------------------
-// wave helpers
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int32_t wave_incl_scan(int32_t x) {
-    const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    return x;
-}
-__device__ __forceinline__ int32_t wave_sum(int32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1, 64); }
-__device__ __forceinline__ uint32_t shfl_down1(uint32_t v) { return (uint32_t)__shfl_down((int)v, 1, 64); }
-// a wave-uniform 64-bit value in scalar registers (the compiler cannot always
-// tell; a buffer resource built from a vector value costs a waterfall loop)
-__device__ __forceinline__ uint64_t uni64(uint64_t x) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-    return (uint64_t)hi << 32 | lo;
-}
-
-#define WAVE_SYNC()                                                    \
-    do {                                                               \
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");         \
-        __builtin_amdgcn_wave_barrier();                               \
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");         \
-    } while (0)
-
-// Words of a tile through a buffer resource over the readable words: loads
-// past the payload return 0 (never read as stream bits).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t fs_rsrc(const uint32_t *g, uint64_t w0, uint64_t nok) {
-    const uint64_t left = nok > w0 ? nok - w0 : 0u;
-    const uint32_t nbytes = left > 0x3fffffffull ? 0xfffffffcu : (uint32_t)left * 4u;
-    return __builtin_amdgcn_make_buffer_rsrc((void *)(g + w0), 0, (int)nbytes, 0x00020000);
-}
-// SW words from word offset wo of the resource
-#ifndef HH_LD_CPOL
-#define HH_LD_CPOL 0          // payload loads' cache policy bits (2: nt)
-#endif
-template <uint32_t SW>
-__device__ __forceinline__ void fs_load(uint32_t *v, __amdgpu_buffer_rsrc_t rs, uint32_t wo) {
-    if (SW % 4 == 0) {
-#pragma unroll
-        for (uint32_t k = 0; k < SW; k += 4) {
-            const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, HH_LD_CPOL));
-            v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
-        }
-    } else {
-#pragma unroll
-        for (uint32_t k = 0; k < SW; k++) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * (wo + k)), 0, 0);
-    }
-}
-
-// byte k / bits [q, q+n) of a region held in registers (compile-time k, q)
-template <uint32_t SW>
-__device__ __forceinline__ uint32_t rbyte(const uint32_t *w, uint32_t k) {
-    return __builtin_amdgcn_ubfe(w[k >> 2], 8 * (k & 3), 8);
-}
-template <uint32_t SW>
-__device__ __forceinline__ uint32_t rbits(const uint32_t *w, uint32_t q, uint32_t n) {
-    const uint32_t i = q >> 5, o = q & 31;
-    if (o + n <= 32 || i + 1 >= SW) return __builtin_amdgcn_ubfe(w[i], o, n);
-    return __builtin_amdgcn_alignbit(w[i + 1], w[i], o) & ((1u << n) - 1u);
-}
-// bits [q, q+N) of a region times 2^SH: a byte offset into a table row
-// (compile-time q)
-template <uint32_t SW, uint32_t N, uint32_t SH>
-__device__ __forceinline__ uint32_t winsh(const uint32_t *w, uint32_t q) {
-    constexpr uint32_t M = ((1u << N) - 1u) << SH;
-    if (q < SH) return (w[0] << (SH - q)) & M;
-    const uint32_t p = q - SH, i = p >> 5, o = p & 31;
-    if (o + N + SH <= 32 || i + 1 >= SW) return (w[i] >> o) & M;
-    return __builtin_amdgcn_alignbit(w[i + 1], w[i], o) & M;
-}
-// bits [q, q+K) of a region times 8: a byte offset into a row of the
-// emission table
-template <uint32_t SW, uint32_t K>
-__device__ __forceinline__ uint32_t win8(const uint32_t *w, uint32_t q) { return winsh<SW, K, 3>(w, q); }
-// the same bits at bit 3 and up, the bits above them unmasked (the caller
-// inserts them with a bit-field insert)
-template <uint32_t SW, uint32_t K>
-__device__ __forceinline__ uint32_t win8raw(const uint32_t *w, uint32_t q) {
-    if (q < 3) return w[0] << (3 - q);
-    const uint32_t p = q - 3, i = p >> 5, o = p & 31;
-    if (o + K + 3 <= 32 || i + 1 >= SW) return w[i] >> o;
-    return __builtin_amdgcn_alignbit(w[i + 1], w[i], o);
-}
-// the LDS byte address of the emission entry for the step's K bits at q from
-// the high word of the previous entry (its row at bits >= 8, 8 x its symbols
-// at bits 3..5, bits 0..2 zero; hh_fsm.h): one bit-field insert
-template <uint32_t SW, uint32_t K>
-__device__ __forceinline__ uint32_t et_addr(uint32_t hi, const uint32_t *w, uint32_t q) {
-    constexpr uint32_t M = ((1u << K) - 1u) << 3;
-    return (win8raw<SW, K>(w, q) & M) | (hi & ~M);
-}
-// bit q of a region held in registers, q not a compile-time constant (rare paths)
-template <uint32_t SW>
-__device__ __forceinline__ uint32_t rbit_dyn(const uint32_t *w, uint32_t q) {
-    uint32_t x = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < SW; k++) x = (q >> 5) == k ? w[k] : x;
-    return (x >> (q & 31)) & 1u;
-}
 
 // The count table at LDS address 0: CB-bit steps (8 for trees of <= 127
 // states, 7 above: hh_fsm.h).  A state is carried as its row's byte offset
@@ -311,7 +82,6 @@ struct CntFmt {
 // (the kernels using the count table declare no static LDS: the dynamic
 // LDS, and with it the table, starts at address 0, and the lookup address
 // is the AND-OR alone -- v_and_or_b32, no base add)
-typedef const uint16_t __attribute__((address_space(3))) *lds_u16p;
 template <uint32_t CB>
 __device__ __forceinline__ uint32_t ct_at(const uint8_t *, uint32_t row, uint32_t off) {
     return *(lds_u16p)(uintptr_t)((row & CntFmt<CB>::RM) | off);
@@ -343,17 +113,11 @@ struct HeadGeo {
     static constexpr uint32_t HWL = (S - CB * HS) / 32;
 };
 
-// The count chain of region j from state s.  IL: the NEXT tile's head chain
-// (*hg, from the root over the last HS steps of region j of that tile -- the
-// full head, G = CB * HS -- words wn) runs interleaved with it, head step h
-// after count step h * NS / HS: two independent chains of LDS lookups in
-// flight instead of one.
-template <uint32_t SW, bool TAIL, uint32_t CB, bool IL = false>
+// The count chain of region j from state s.
+template <uint32_t SW, bool TAIL, uint32_t CB>
 __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_t *b1, const uint32_t *w,
-                                               uint32_t s, uint32_t lim, uint32_t *n, const uint32_t *wn = nullptr,
-                                               uint32_t *hg = nullptr) {
-    typedef HeadGeo<SW, CB> HG;
-    uint32_t c = 0, h = 0, ep = 0;
+                                               uint32_t s, uint32_t lim, uint32_t *n) {
+    uint32_t c = 0, ep = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 32 * SW / CB; k++) {
         if (!TAIL || CB * k + CB <= lim) {
@@ -365,31 +129,12 @@ __device__ __forceinline__ uint32_t cnt_region(const uint8_t *lds, const uint32_
             // step but left to the scheduler, the adds sink to the end of
             // the chain and every step's entry stays live -- 32 registers,
             // the difference between 24 and 32 waves per CU)
-            if (HH_CNT_DADD) {
-                c += ep;
-                asm volatile("" : "+v"(c));
-                ep = e;
-            } else {
-                c += e;
-                asm volatile("" : "+v"(c));
-            }
-        }
-        if (IL) {
-#pragma unroll
-            for (uint32_t i = 0; i < HG::HS; i++)
-                if (i * HG::NS / HG::HS == k) {
-                    const uint32_t q = HG::NS - HG::HS + i;      // (the head's step index in its region)
-                    // (IL: G = CB * HS, the full head.  The step's offset
-                    // opaque: merged into the address, it costs 4 VALU
-                    // instead of an extract and an AND-OR)
-                    uint32_t o = cstep<SW, CB>(wn, q);
-                    asm volatile("" : "+v"(o));
-                    h = ct_at<CB>(lds, h, o);
-                }
+            c += ep;
+            asm volatile("" : "+v"(c));
+            ep = e;
         }
     }
-    if (IL) *hg = h & CntFmt<CB>::RM;
-    if (HH_CNT_DADD) c += ep;
+    c += ep;
     c &= CntFmt<CB>::CM;
     s &= CntFmt<CB>::RM;
     if (TAIL)
@@ -412,7 +157,7 @@ __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *
 #pragma unroll
     for (uint32_t k = 0; k < 32 * SW / CB; k++) {
         if (go && (!TAIL || CB * k + CB <= lim)) {
-            if (!HH_WALK_MASK || A != B) {
+            if (A != B) {
                 const uint32_t x = cstep<SW, CB>(w, k);
                 const uint32_t ea = ct_at<CB>(lds, A, x), eb = ct_at<CB>(lds, B, x);
                 A = ea & RM;
@@ -420,7 +165,7 @@ __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *
                 d += (int32_t)(ea & 15u) - (int32_t)(eb & 15u);
             }
         }
-        if ((k & HH_WALK_CHK) == HH_WALK_CHK && go) go = __ballot(A != B) != 0;
+        if ((k & 1u) == 1u && go) go = __ballot(A != B) != 0;   // (every second step)
     }
     if (TAIL) {
         for (uint32_t q = lim / CB * CB; q < lim && A != B; q++) {
@@ -440,7 +185,7 @@ __device__ __forceinline__ void walk_region(const uint8_t *lds, const uint32_t *
 // (hh_fsm_algo.h), run by the whole wave on uniform chains with the region's
 // words in registers, the next region's loaded during the walk.  (Lane 0
 // alone reading every window from global memory: ~25 us per fix, the
-// slowest waves of a 64 MiB count -- per-wave spans of the HH_WSPAN build.)
+// slowest waves of a 64 MiB count -- round 5's per-wave end-time stamps.)
 // T1: the next tile's first bit (a whole word).  Out of line, by value.
 struct CntFix {
     uint32_t f[FX_W];
@@ -490,23 +235,14 @@ __host__ __device__ constexpr uint32_t cnt_tab_bytes(uint32_t ns, uint32_t cb) {
 // The count launches' LDS: the tables, then k_cntm's chunk counter (16 B)
 __host__ __device__ constexpr uint32_t cnt_ctr_off(uint32_t ns, uint32_t cb) { return cnt_tab_bytes(ns, cb); }
 
-// One tile: w = region j's words, nx = region j+1's (lane 63: the next
-// tile's region 0), or (HH_CNT_PNX == 0) loaded here when some lane walks --
-// with a 128-bit head most tiles have no walk, and registers held across the
-// count for the rare walk cost occupancy.
-#ifdef HH_DIAG
-#define CDIAG_ARGS , uint64_t *cg_acc, uint64_t *cg_n, uint64_t &cg_t
-#define CDIAG_PASS , cg_acc, cg_n, cg_t
-#else
-#define CDIAG_ARGS
-#define CDIAG_PASS
-#endif
+// One tile: w = region j's words; region j+1's are loaded here when some
+// lane walks -- with a 128-bit head most tiles have no walk, and registers
+// held across the count for the rare walk cost occupancy.
 // hin: lane 0's guess for region 0 when the caller has it (the previous
 // tile's lane-63 head, same wave: tiles in order), else HIN_NONE (computed
 // here from pv, the 16 bytes before the tile).  Returns lane 63's head (the
 // next tile's region-0 guess), as a row.
 #define HIN_NONE 0xffffffffu
-typedef uint32_t __attribute__((address_space(3))) *lds_u32p;
 // decodeallbits: lane j's guess gs for region j+1's entering state (a chain
 // from the root over the last G bits of region j) and (hin == HIN_NONE) lane
 // 0's guess hp for its own region 0: the same head over the previous
@@ -543,15 +279,10 @@ __device__ __forceinline__ void cnt_heads(const uint8_t *lds, const uint32_t *w,
     }
     gs &= RM;
 }
-// IL: the heads of this tile are given (gs_il: lane j's guess for region
-// j+1, hin lane 0's for region 0 -- computed while the previous tile was
-// counted), and the next tile's heads are computed here, interleaved with
-// this tile's count, from its words wn -> *gsn.
-template <uint32_t SW, bool TAIL, uint32_t CB, bool IL = false>
+template <uint32_t SW, bool TAIL, uint32_t CB>
 __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_view &F, const uint32_t *__restrict__ g,
                                              const FsmGeo &geo, const FsmWork &wk, uint64_t t, const uint32_t *w,
-                                             const uint32_t *nx, const uint32_t *pv, uint32_t hin CDIAG_ARGS,
-                                             uint32_t gs_il = 0, const uint32_t *wn = nullptr, uint32_t *gsn = nullptr) {
+                                             const uint32_t *pv, uint32_t hin) {
     constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS;
     const uint32_t j = threadIdx.x & 63u;
     const uint64_t TB = (uint64_t)NR * S, T0 = t * TB;
@@ -567,26 +298,16 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
     // decodeallbits: the guess for region j+1 (a chain started at the root G
     // bits before it), then region j from the guess lane j-1 made for it
     uint32_t gs = 0, hp = 0;
-#ifndef HH_XP_NOHEAD
-#define HH_XP_NOHEAD 0        // (timing experiments only: results are wrong)
-#endif
-    if (IL) {
-        gs = gs_il;
-        hp = hin;
-    } else if (geo.G && !HH_XP_NOHEAD) {
-        cnt_heads<SW, CB>(lds, w, pv, geo.G, hin, gs, hp);
-    }
-    CDIAG_STAMP(0);
+    if (geo.G) cnt_heads<SW, CB>(lds, w, pv, geo.G, hin, gs, hp);
     const uint32_t gup = shfl_up1(gs);              // (cross-lane ops with every lane active)
     const uint32_t sp = j ? gup : (t == 0 ? geo.in_state << RS : hp);
     uint32_t n;
-    uint32_t X = cnt_region<SW, TAIL, CB, IL>(lds, F.b1, w, sp, lim, &n, wn, gsn);   // region j's exit (given its entry)
+    uint32_t X = cnt_region<SW, TAIL, CB>(lds, F.b1, w, sp, lim, &n);   // region j's exit (given its entry)
     // the stream ends in region j / in region j+1: the tail rule counts a
     // chain that is not at the root there (fsm_region, fsm_walk2)
     const bool endj = TAIL && lim > 0 && R + lim == geo.bits;
     const bool endn = TAIL && limn > 0 && R + S + limn == geo.bits;
     if (endj && X != 0) n += 1;
-    CDIAG_STAMP(1);
 
     // makebigtable: where region j's exit differs from the entry assumed for
     // region j+1 (E), lane j walks region j+1 with both chains; their count
@@ -597,34 +318,22 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
     uint32_t E = gs;                                // (lane 63: the next tile's region 0, guessed alike)
     int32_t d = 0;
     bool lost = false;                              // lane 63: not met in the next tile's region 0
-#ifndef HH_XP_NOWALK
-#define HH_XP_NOWALK 0        // (timing experiments only: results are wrong)
-#endif
     uint32_t nv[SW];
     bool have_nv = false;
-    for (int round = 0; round < (HH_XP_NOWALK ? 0 : NR); round++) {
+    for (int round = 0; round < NR; round++) {
         const bool want = X != E && limn > 0 && (j < 63 || has_next);
         if (__ballot(want) == 0) break;
-        CDIAG_COUNT(1, round == 0);
-        CDIAG_COUNT(2, 1);
         uint32_t A = X, B = want ? E : X;           // (not walking: A == B, no change)
         int32_t dd = 0;
-        if (HH_CNT_PNX == 1) {
-            if (round == 0) {
+        if (round == 0) {
 #pragma unroll
-                for (uint32_t k = 0; k < SW; k++) nv[k] = nx[k];
-            }
-        } else {
-            if (round == 0) {
-#pragma unroll
-                for (uint32_t k = 0; k < SW; k++) nv[k] = 0u;
-            }
-            if (want && !have_nv) {
-                // region j+1's words, loaded by the walking lanes only (the
-                // others' lookups are masked off; their words are not used)
-                fs_load<SW>(nv, fs_rsrc(g, uni64(t) * TB / 32, geo.nwords), (j + 1) * SW);
-                have_nv = true;
-            }
+            for (uint32_t k = 0; k < SW; k++) nv[k] = 0u;
+        }
+        if (want && !have_nv) {
+            // region j+1's words, loaded by the walking lanes only (the
+            // others' lookups are masked off; their words are not used)
+            fs_load<SW>(nv, fs_rsrc(g, uni64(t) * TB / 32, geo.nwords), (j + 1) * SW);
+            have_nv = true;
         }
         // (opaque per round: the byte offsets of the walk are not hoisted out
         // of the rounds loop into 4 x SW live registers)
@@ -646,8 +355,6 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
         if (j > 0 && dp) X = xa;
     }
 
-    CDIAG_STAMP(2);
-    CDIAG_COUNT(0, 1);
     // records: region j entered in the state lane j-1 assumed last
     const uint32_t Eup = shfl_up1(E), dup = shfl_up1((uint32_t)d);
     const uint32_t ent = (j ? Eup : sp) >> RS;
@@ -691,12 +398,9 @@ __device__ __forceinline__ uint32_t cnt_tile(const uint8_t *lds, const hh_fsm_vi
     wk.fxs[t + 1] = fsum;
     wk.xs[t] = x | fail << 31;                        // (bit 31: chains that did not meet, k_fscan reports it)
     return (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
-    CDIAG_STAMP(3);
 }
 
-#ifndef HH_CNT_WAVES
-#define HH_CNT_WAVES 8        // k_cnt: waves per SIMD the register budget is cut for (32 per CU: 2 workgroups of 16)
-#endif
+#define CNT_WAVES 8           // k_cnt: waves per SIMD the register budget is cut for (32 per CU: 2 workgroups of 16)
 // The count pass over tiles [t0, t1) as workgroup blk of nblk with CWX waves
 // each (k_cnt; and the tail tiles run by the last workgroups of k_cntm's
 // launch, instead of a launch of their own after it).
@@ -726,89 +430,24 @@ __device__ __forceinline__ void cnt_run(const uint32_t *__restrict__ g, const Fs
     uint32_t t = TAIL ? (uint32_t)t0 + gw : (uint32_t)t0 + gw * run;
     const uint32_t tend = TAIL ? te : (t + run < te ? t + run : te);
     const uint32_t tstep = TAIL ? nwv : 1u;
-    // the next tile's words are loaded one tile ahead: region j's and region
-    // j+1's (used only by walks; waiting for them at the walk, behind the
-    // previous tile's stores, cost as much as the walks themselves)
+    // the next tile's words are loaded one tile ahead
     // (and the HB bytes before the tile, for lane 0's head: lane i loads word
     // i -- a scalar load would be waited for by every LDS wait of the tile,
     // since scalar loads return out of order and share the LDS counter)
     constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
-    uint32_t pw[SW], pn[SW] = {}, ppv = 0;
+    uint32_t pw[SW], ppv = 0;
     auto prefetch = [&](uint32_t tt, bool with_pv) {
         tt = (uint32_t)__builtin_amdgcn_readfirstlane((int)tt);
         const uint64_t tw = (uint64_t)tt * TB / 32, pa = tw >= HB / 4 ? tw - HB / 4 : 0u;   // (tile 0: unused)
         const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tw, geo.nwords);
         // (the lane id recomputed here: the register budget has no room to
         // keep the load offsets live across the tile)
-        uint32_t ln;
-        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+        const uint32_t ln = lane_id();
         fs_load<SW>(pw, rs, ln * SW);
-        if (HH_CNT_PNX) fs_load<SW>(pn, rs, (ln + 1) * SW);
         if (with_pv) ppv = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (ln % (HB / 4))), 0, 0);
     };
-    CDIAG_DECL
     if (t == 0 && j < FX_W) wk.fx[j] = 0u;           // (tile 0 has no predecessor to correct it)
     if (t == 0 && j == 0) wk.fxs[0] = 0;
-    if (!TAIL && HH_CNT_IL && !HH_CNT_PNX && geo.G == CB * HeadGeo<SW, CB>::HS) {
-        // Interleaved heads: tile t+1's heads run beside tile t's counts, so
-        // a lane has two independent chains of lookups in flight.  The head
-        // reads a region's words [HWL, SW) only: those of tile t+1 are loaded
-        // two tiles ahead, the rest one tile ahead.
-        constexpr uint32_t HWL = HeadGeo<SW, CB>::HWL;
-        uint32_t wc[SW], wn[SW], wnn[SW];       // (wn, wnn: words [HWL, SW) only; wn's [0, HWL) loaded into wc's)
-        auto load_words = [&](uint32_t *v, uint32_t tt, uint32_t a, uint32_t b) {
-            tt = (uint32_t)__builtin_amdgcn_readfirstlane((int)tt);
-            const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, (uint64_t)tt * TB / 32, geo.nwords);
-            uint32_t ln;
-            asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-            if (SW % 4 == 0 && a % 4 == 0 && b % 4 == 0) {
-#pragma unroll
-                for (uint32_t k = 0; k < SW; k += 4)
-                    if (k >= a && k < b) {
-                        const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (ln * SW + k)), 0, 0));
-                        v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
-                    }
-            } else {
-#pragma unroll
-                for (uint32_t k = 0; k < SW; k++)
-                    if (k >= a && k < b) v[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(4u * (ln * SW + k)), 0, 0);
-            }
-        };
-        if (t < tend) {
-            const uint32_t tn = t + 1 < tend ? t + 1 : t;
-            load_words(wc, t, 0, SW);
-            load_words(wn, tn, HWL, SW);
-            uint32_t pv[HB / 4];
-            {
-                const uint64_t tw = (uint64_t)t * TB / 32, pa = tw >= HB / 4 ? tw - HB / 4 : 0u;   // (tile 0: unused)
-                const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (j % (HB / 4))), 0, 0);
-#pragma unroll
-                for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, i);
-            }
-            // the run's first tile: its heads (and lane 0's) on their own
-            uint32_t gs = 0, hp = 0;
-            cnt_heads<SW, CB>(smem, wc, pv, geo.G, HIN_NONE, gs, hp);
-            hp = (uint32_t)__builtin_amdgcn_readfirstlane((int)hp);
-            for (; t < tend; t++) {
-                t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-                const uint32_t tn = t + 1 < tend ? t + 1 : t, tnn = t + 2 < tend ? t + 2 : tn;
-                if (HWL) load_words(wn, tn, 0, HWL);        // tile t+1's words [0, HWL) (its [HWL, SW) arrived)
-                load_words(wnn, tnn, HWL, SW);
-                uint32_t gsn = 0;
-                const uint32_t h63 = cnt_tile<SW, false, CB, true>(smem, F, g, geo, wk, (uint64_t)t, wc, wc, nullptr, hp CDIAG_PASS,
-                                                                   gs, wn, &gsn);
-                hp = (uint32_t)__builtin_amdgcn_readfirstlane((int)h63);
-                gs = gsn;
-#pragma unroll
-                for (uint32_t k = 0; k < SW; k++) {
-                    wc[k] = wn[k];
-                    if (k >= HWL) wn[k] = wnn[k];
-                }
-            }
-        }
-        CDIAG_FLUSH(wk.dbg);
-        return;
-    }
     // The bytes before a tile (pv) are needed by the first tile of a run only
     // (TAIL: every tile): read once before the loop, the loop's loads are the
     // words alone -- reading pv in the loop had every tile wait for all of
@@ -821,25 +460,21 @@ __device__ __forceinline__ void cnt_run(const uint32_t *__restrict__ g, const Fs
     }
     for (; t < tend; t += tstep) {
         t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-        uint32_t w[SW], nx[SW];
+        uint32_t w[SW];
 #pragma unroll
-        for (uint32_t k = 0; k < SW; k++) {
-            w[k] = pw[k];
-            nx[k] = pn[k];
-        }
+        for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
         if (TAIL) {
 #pragma unroll
             for (uint32_t i = 0; i < HB / 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
         }
         prefetch(t + tstep < tend ? t + tstep : t, TAIL);
-        const uint32_t h63 = cnt_tile<SW, TAIL, CB>(smem, F, g, geo, wk, (uint64_t)t, w, nx, pv, hin CDIAG_PASS);
+        const uint32_t h63 = cnt_tile<SW, TAIL, CB>(smem, F, g, geo, wk, (uint64_t)t, w, pv, hin);
         hin = TAIL ? HIN_NONE : (uint32_t)__builtin_amdgcn_readfirstlane((int)h63);
     }
-    CDIAG_FLUSH(wk.dbg);
 }
 
 template <uint32_t SW, bool TAIL, uint32_t CB>
-__global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_WAVES, 8))) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+__global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(CNT_WAVES, 8))) void k_cnt(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint64_t t0, uint64_t t1) {
     cnt_run<SW, TAIL, CB, CW>(g, geo, tab, wk, t0, t1, blockIdx.x, gridDim.x);
 }
@@ -864,27 +499,14 @@ __global__ __launch_bounds__(64 * CW) __attribute__((amdgpu_waves_per_eu(HH_CNT_
 // cntm_waves(M) waves per SIMD (a lane holds its whole span of M regions:
 // more than k_cnt's 64 VGPRs).  M = 2: 24 waves per CU in 3 workgroups of 8
 // (80 VGPRs); M = 4: 20 in 2 of 10 (96 VGPRs); each workgroup its tables.
-#ifndef HH_CNTM2_CW
-#define HH_CNTM2_CW 8
-#endif
-#ifndef HH_CNTM2_WAVES
-#define HH_CNTM2_WAVES 6
-#endif
-#ifndef HH_CNTM7_CW
-#define HH_CNTM7_CW 12
-#endif
 // (cb 7: 65 KB count tables for 255 states -- two workgroups per CU, of 12
 // waves: byte alphabet count 0.51 -> 0.43 ms against 8)
 __host__ __device__ constexpr uint32_t cntm_cw(uint32_t m, uint32_t cb = 8) {
-    return m >= 4 ? 10u : cb == 7 ? HH_CNTM7_CW : HH_CNTM2_CW;
+    return m >= 4 ? 10u : cb == 7 ? 12u : 8u;
 }
-__host__ __device__ constexpr uint32_t cntm_waves(uint32_t m) { return m >= 4 ? 5u : HH_CNTM2_WAVES; }
-#ifndef HH_CNT_CKDIV
-#define HH_CNT_CKDIV 4        // chunks of at most wrun / (waves x CKDIV) tiles, at least 1 (0: wrun / waves)
-#endif
-#ifndef HH_CNT_CHUNK
-#define HH_CNT_CHUNK 4        // k_cntm: count tiles per chunk a wave takes from its workgroup's counter
-#endif
+__host__ __device__ constexpr uint32_t cntm_waves(uint32_t m) { return m >= 4 ? 5u : 6u; }
+#define CNT_CKDIV 4           // chunks of at most wrun / (waves x CKDIV) tiles, at least 1
+#define CNT_CHUNK 4           // k_cntm: count tiles per chunk a wave takes from its workgroup's counter
 #ifndef HH_CNT_M
 #define HH_CNT_M 2            // regions per lane of the count pass: 2, 4 (k_cntm) or 1 (k_cnt; HH_CNT_M=n overrides)
 #endif
@@ -933,59 +555,6 @@ __device__ __noinline__ CntmWalk cntm_walk(const uint32_t *b1, const uint32_t *_
     return CntmWalk{a, dsum, met ? 1u : 0u};
 }
 
-// HH_WALK_REG: the same walk on the successor's records held in registers
-// (rc: lane j+1's record words, as its count left them or as this lane's
-// earlier rounds rewrote them -- lane j is the only lane that rewrites lane
-// j+1's records), the records stored once after the walks: no record reads,
-// no wait for the tile's stores before a walk.  The successor's words: both
-// regions' loads issued at once.
-template <uint32_t M>
-struct CntmWalkR {
-    uint32_t A;
-    int32_t d;
-    uint32_t met;
-    uint32_t rc[M];
-};
-template <uint32_t SW, uint32_t CB, uint32_t M>
-__device__ __noinline__ CntmWalkR<M> cntm_walk_reg(const uint32_t *b1, const uint32_t *__restrict__ g, uint64_t nwords,
-                                                   uint64_t q0, bool want, uint32_t A, uint32_t B0, CntmWalkR<M> in) {
-    constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS;
-    bool met = !want;
-    uint32_t a = A, b = B0;
-    int32_t dsum = 0;
-    uint32_t nv[M][SW];
-#pragma unroll
-    for (uint32_t r = 0; r < M; r++)
-#pragma unroll
-        for (uint32_t k = 0; k < SW; k++) nv[r][k] = 0u;
-    if (!met) {
-#pragma unroll
-        for (uint32_t r = 0; r < M; r++) fs_load<SW>(nv[r], fs_rsrc(g, (q0 + r) * SW, nwords), 0);
-    }
-#pragma unroll
-    for (uint32_t r = 0; r < M; r++) {
-        if (__ballot(!met) == 0) break;
-        if (r > 0 && !met) b = fsm_rec_ent(in.rc[r]) << RS;
-#pragma unroll
-        for (uint32_t k = 0; k < SW; k++) asm volatile("" : "+v"(nv[r][k]));
-        uint32_t aa = met ? 0u : a, bb = met ? 0u : b;
-        int32_t dd = 0;
-        walk_region<SW, false, CB>(nullptr, b1, nv[r], aa, bb, dd, S);
-        if (!met) {
-            in.rc[r] = fsm_rec(a >> RS, (uint32_t)((int32_t)fsm_rec_cnt(in.rc[r]) + dd));
-            dsum += dd;
-            met = aa == bb;
-            a = aa;
-        }
-    }
-    in.A = a;
-    in.d = dsum;
-    in.met = met ? 1u : 0u;
-    return in;
-}
-#ifndef HH_WALK_REG
-#define HH_WALK_REG 0         // k_cntm: the walks on records held in registers (above; measured slower: count 0.395 -> 0.42 ms)
-#endif
 
 template <uint32_t SW, uint32_t CB, uint32_t M>
 __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_per_eu(cntm_waves(M), 8))) void k_cntm(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
@@ -1000,7 +569,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         cnt_run<SW, true, CB, CWM>(g, geo, tab, wk, u0, u1, blockIdx.x, ntb);
         return;
     }
-    WSPAN_START(0);
     extern __shared__ __align__(16) uint8_t smem[];
     constexpr uint32_t S = 32 * SW, RS = CntFmt<CB>::RS, LG = 64 / M;   // LG: lanes per emission tile
     constexpr uint32_t HB = 4 * SW < HH_FSM_GMAX / 8 ? 4 * SW : HH_FSM_GMAX / 8;
@@ -1016,24 +584,19 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     if (tid == 0) *(lds_u32p)(uintptr_t)ctr = 0u;
     __syncthreads();
     const hh_fsm_view F = {(const uint16_t *)smem, s_b1, s_ts, CB};
-    WSPAN_FILLED();
     // Each workgroup counts a contiguous range of count tiles, its waves
     // taking chunks of ck tiles in turn from the workgroup's LDS counter; a
     // wave counts a chunk's tiles in order -- lane 0's entry guess of a tile:
     // the previous tile's lane-63 head; of a chunk's first, a head over the
     // bytes before it.  (Equal runs per wave: the workgroup's waves ended up
-    // to 50 us apart, per-wave end times of the HH_WSPAN build.  Chunks from
+    // to 50 us apart in round 5's per-wave end-time stamps.  Chunks from
     // one device-scope counter per XCD instead: count 0.40 -> 0.42 ms.)
-    // ck: HH_CNT_CHUNK tiles, or fewer where a workgroup's range holds fewer
-    // than HH_CNT_CKDIV chunks per wave (small streams: 128 MiB count 0.070
+    // ck: CNT_CHUNK tiles, or fewer where a workgroup's range holds fewer
+    // than CNT_CKDIV chunks per wave (small streams: 128 MiB count 0.070
     // -> 0.063 ms against one chunk per wave)
     const uint32_t nwg = gridDim.x - ntb, wgi = blockIdx.x - ntb, ce = (uint32_t)c1;
     const uint32_t wrun = ((uint32_t)(c1 - c0) + nwg - 1) / nwg;
-#if HH_CNT_CKDIV
-    const uint32_t ck = max(1u, min((uint32_t)HH_CNT_CHUNK, wrun / (CWM * HH_CNT_CKDIV)));
-#else
-    const uint32_t ck = min((uint32_t)HH_CNT_CHUNK, (wrun + CWM - 1) / CWM);
-#endif
+    const uint32_t ck = max(1u, min((uint32_t)CNT_CHUNK, wrun / (CWM * CNT_CKDIV)));
     const uint32_t wc0 = (uint32_t)c0 + wgi * wrun < ce ? (uint32_t)c0 + wgi * wrun : ce;
     const uint32_t wc1 = wc0 + wrun < ce ? wc0 + wrun : ce;
     const uint32_t nchunk = (wc1 - wc0 + ck - 1) / ck;
@@ -1048,7 +611,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     }
     uint32_t kc = claim();
     if (kc >= nchunk) {
-        WSPAN_END(wk.dbg, 0);
         return;
     }
     uint32_t c = wc0 + kc * ck, cend = c + ck < wc1 ? c + ck : wc1;
@@ -1064,7 +626,7 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
 #pragma unroll
             for (uint32_t k = 0; k < SW; k += 4)
                 if (k >= a && k < b) {
-                    const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, HH_LD_CPOL));
+                    const u32x4 q = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(4u * (wo + k)), 0, 0));
                     v[k] = q.x; v[k + 1] = q.y; v[k + 2] = q.z; v[k + 3] = q.w;
                 }
         } else {
@@ -1094,7 +656,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
     __builtin_amdgcn_s_waitcnt(VMCNT0);
     for (;;) {
         c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
-        WSPAN_MARK();
         const uint64_t Q0 = (uint64_t)c * (64u * M);     // the tile's first region
         // the next tile: this chunk's next, else the next chunk's first
         const bool last = c + 1 >= cend;
@@ -1117,7 +678,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
                 cnt_heads<SW, CB, false>(smem, span + (M - 1) * SW, nullptr, geo.G, hin, gs, hp);
             }
         }
-        WSPAN_PH(0);
         const uint32_t gup = shfl_up1(gs);
         const uint32_t sp = j ? gup : (c == 0 ? geo.in_state << RS : hp);
         // the lane's regions in order (records through a buffer resource on
@@ -1125,7 +685,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         const __amdgpu_buffer_rsrc_t rrs =
             __builtin_amdgcn_make_buffer_rsrc((void *)(wk.rec + Q0), 0, (int)(64u * M * 4u), 0x00020000);
         uint32_t s = sp, nsum = 0;
-        CntmWalkR<M> wr;
 #pragma unroll
         for (uint32_t r = 0; r < M; r++) {
             uint32_t w[SW];
@@ -1138,19 +697,11 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
             }
             uint32_t n;
             const uint32_t X = cnt_region<SW, false, CB>(smem, F.b1, w, s, S, &n);
-            if (HH_WALK_REG) wr.rc[r] = fsm_rec(s >> RS, n);   // (lane j's own; lane j-1's view below)
-            else __builtin_amdgcn_raw_buffer_store_b32(fsm_rec(s >> RS, n), rrs, (int)(4u * (j * M + r)), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(fsm_rec(s >> RS, n), rrs, (int)(4u * (j * M + r)), 0, 0);
             nsum += n;
             s = X;
         }
-        WSPAN_PH(1);
         uint32_t X = s, E = gs;
-        uint32_t own[M];                                 // (lane 0 stores its own records)
-#pragma unroll
-        for (uint32_t r = 0; r < M; r++) {
-            own[r] = wr.rc[r];
-            if (HH_WALK_REG) wr.rc[r] = shfl_down1(wr.rc[r]);   // lane j: lane j+1's records
-        }
 
         // makebigtable: walks into the successor's regions (lane 63: into the
         // next tile's region 0, its corrections in fx as in k_cnt)
@@ -1159,24 +710,16 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         for (int round = 0; round < NR; round++) {
             const bool want = X != E && (j < 63 || has_next);
             if (__ballot(want) == 0) break;
-            WSPAN_EVENT(48);
             // (the tile's records -- and the last round's rewrites -- reached
             // memory: walks read them back)
-            if (!HH_WALK_REG) __builtin_amdgcn_s_waitcnt(VMCNT0);
+            __builtin_amdgcn_s_waitcnt(VMCNT0);
             uint32_t A = X;
             bool met;
             if (j < 63) {
-                if (HH_WALK_REG) {
-                    wr = cntm_walk_reg<SW, CB, M>(F.b1, g, geo.nwords, Q0 + (uint64_t)(j + 1) * M, want, A, E, wr);
-                    A = wr.A;
-                    dsum += wr.d;
-                    met = wr.met != 0;
-                } else {
-                    const CntmWalk cw = cntm_walk<SW, CB, M>(F.b1, g, geo.nwords, wk.rec, Q0 + (uint64_t)(j + 1) * M, want, A, E);
-                    A = cw.A;
-                    dsum += cw.d;
-                    met = cw.met != 0;
-                }
+                const CntmWalk cw = cntm_walk<SW, CB, M>(F.b1, g, geo.nwords, wk.rec, Q0 + (uint64_t)(j + 1) * M, want, A, E);
+                A = cw.A;
+                dsum += cw.d;
+                met = cw.met != 0;
             } else {
                 // lane 63: the next tile's region 0 (its own record not written yet)
                 uint32_t nv[SW];
@@ -1200,15 +743,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
             const uint32_t dp = shfl_up1(deep ? 1u : 0u), xa = shfl_up1(A);
             if (j > 0 && dp) X = xa;
         }
-        if (HH_WALK_REG) {
-            // the records: lane j's as lane j-1 left them (lane 0's its own)
-#pragma unroll
-            for (uint32_t r = 0; r < M; r++) {
-                const uint32_t up = shfl_up1(wr.rc[r]);
-                __builtin_amdgcn_raw_buffer_store_b32(j ? up : own[r], rrs, (int)(4u * (j * M + r)), 0, 0);
-            }
-        }
-        WSPAN_PH(2);
         // per emission tile (LG lanes): counts with the walks' corrections
         const uint32_t recv = shfl_up1((uint32_t)dsum);
         int32_t v = (int32_t)nsum + (j ? (int32_t)recv : 0);
@@ -1232,7 +766,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
                 const uint32_t h63 = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63) >> RS;
                 const CntFix fo = cnt_fix_wave<SW, CB>(F.b1, g, geo.nwords, geo.bits, (Q0 + 64u * M) * S, x, h63);
                 const uint32_t *f = fo.f, ok = fo.ok;
-                WSPAN_EVENT(58);
 #pragma unroll
                 for (int i = 0; i < FX_W; i++) {
                     const uint32_t fv = (uint32_t)__builtin_amdgcn_readlane((int)f[i], 0);
@@ -1252,7 +785,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
         // states leaving the emission tiles (the last one's is the tile's)
         wk.xs[(uint64_t)c * M + grp] = (grp == M - 1 ? x : 0u) | fail << 31;
         hin = (uint32_t)__builtin_amdgcn_readlane((int)gs, 63);
-        WSPAN_PH(3);
         if (!more) break;
         if (last) {
             c = cn;
@@ -1262,7 +794,6 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
             c++;
         }
     }
-    WSPAN_END(wk.dbg, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1272,11 +803,8 @@ __global__ __launch_bounds__(64 * cntm_cw(M, CB)) __attribute__((amdgpu_waves_pe
 // The block totals -> exclusive block bases; totals and states into the
 // result slot (k_fscan1's last block; blk / bmax were stored sc1 by every
 // block, so they are read with sc1 loads -- agent-scope atomic loads -- and
-// no cache write-back or invalidate is needed on either side).
-// (SC1: the bases and the largest tile output stored sc1, for k_emf's own
-// workgroups to read in the same launch -- HH_SCAN_FUSED; s_w, s_mx2, s_fl:
-// 16 words of LDS each)
-template <bool SC1>
+// no cache write-back or invalidate is needed on either side).  s_w, s_mx2,
+// s_fl: 16 words of LDS each.
 __device__ __forceinline__ void fscan_final(const FsmGeo &geo, const FsmWork &wk, uint32_t nblk, uint32_t *res, int64_t *s_w,
                                             int32_t *s_mx2, uint32_t *s_fl) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
@@ -1305,8 +833,7 @@ __device__ __forceinline__ void fscan_final(const FsmGeo &geo, const FsmWork &wk
             tot += s_w[i];
         }
         if (b0 + tid < nblk) {
-            if (SC1) __hip_atomic_store(&wk.blk[b0 + tid], carry + base + x - v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else wk.blk[b0 + tid] = carry + base + x - v;   // (read by k_emf, after this kernel)
+            wk.blk[b0 + tid] = carry + base + x - v;   // (read by k_emf, after this kernel)
         }
         carry += tot;
         __syncthreads();
@@ -1327,8 +854,7 @@ __device__ __forceinline__ void fscan_final(const FsmGeo &geo, const FsmWork &wk
             mx = max(mx, s_mx2[i]);
             fl |= s_fl[i] ? (uint32_t)FF_FAIL : 0u;
         }
-        if (SC1) __hip_atomic_store(&wk.flags[6], (uint32_t)mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else wk.flags[6] = (uint32_t)mx;  // the largest tile output (symbols)
+        wk.flags[6] = (uint32_t)mx;       // the largest tile output (symbols)
         wk.flags[8] = 0u;                 // (the block ticket, for the next decode's k_fscan1)
         const uint32_t lv = geo.ntiles ? wk.xs[geo.ntiles - 1] & 255u : geo.in_state;
         uint32_t en = geo.in_state;
@@ -1351,13 +877,17 @@ __device__ __forceinline__ void fscan_final(const FsmGeo &geo, const FsmWork &wk
 // nothing), the exclusive prefix within the block -> lex, the block total ->
 // blk.  The block that finishes last then scans the block totals
 // (fscan_final): one launch for the whole scan.  The hand-off without fences
-// (MI355X_MICROARCH.md, the sc1 hand-off table, row 1): each block's totals
-// stored sc1 by one lane, that lane's vmcnt(0), then its agent-scope add to
-// a ticket (flags[8]); the block whose add returns nblk - 1 reads them sc1.
-// Block b's part (SCAN_TB threads); returns (uniform) whether it drew the
-// last ticket.  SC1: the prefixes stored sc1 (HH_SCAN_FUSED).  s_tmp, s_mx:
-// SCAN_TB / 64 words of LDS each, s_last one.
-template <bool SC1>
+// is row 1 of MI355X_MICROARCH.md's measured sc1 hand-off table, cell for
+// cell (gfx950 only: hh_fsm_kern.h refuses other targets): each block's
+// totals stored sc1 (agent-scope relaxed atomic stores) by ONE lane, that
+// lane's s_waitcnt vmcnt(0), then its agent-scope add to ONE ticket word
+// (flags[8]); the block whose add returns nblk - 1 -- the last adder, told
+// by the value its add returned -- reads them with sc1 loads (agent-scope
+// atomic loads), its other waves after a workgroup barrier.
+// (test_gpu_parity.py::test_scan_blocks_against_host_prefix checks the bases
+// of a many-block scan.)  Block b's part (SCAN_TB threads); returns (uniform)
+// whether it drew the last ticket.  s_tmp, s_mx: SCAN_TB / 64 words of LDS
+// each, s_last one.
 __device__ __forceinline__ bool fscan_block(const FsmGeo &geo, const FsmWork &wk, uint32_t b, uint32_t nblk, int32_t *s_tmp,
                                             int32_t *s_mx, uint32_t *s_last) {
     const uint64_t t = (uint64_t)b * SCAN_TB + threadIdx.x;
@@ -1382,20 +912,11 @@ __device__ __forceinline__ bool fscan_block(const FsmGeo &geo, const FsmWork &wk
         tot += v;
         mx = max(mx & ~BMAX_FAIL, s_mx[i] & ~BMAX_FAIL) | ((mx | s_mx[i]) & BMAX_FAIL);
     }
-    if (t <= geo.ntiles) {
-        if (SC1) __hip_atomic_store(&wk.lex[t], base + x - c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else wk.lex[t] = base + x - c;
-    }
-    if (SC1) {
-        // (every thread's prefix stored before the block's ticket: k_emf's
-        // workgroups read them in this launch)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    if (t <= geo.ntiles) wk.lex[t] = base + x - c;   // (read by k_emf, after this kernel)
     if (threadIdx.x == 0) {
         __hip_atomic_store(&wk.blk[b], (int64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&wk.bmax[b], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (SC1: this thread's stores only -- see k_emf)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (this thread's stores, before its ticket)
         *s_last = __hip_atomic_fetch_add(&wk.flags[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblk - 1u;
     }
     __syncthreads();
@@ -1407,15 +928,12 @@ __global__ __launch_bounds__(SCAN_TB) void k_fscan1(FsmGeo geo, FsmWork wk, uint
     __shared__ int64_t s_w[16];
     __shared__ int32_t s_mx2[16];
     __shared__ uint32_t s_fl[16];
-    if (fscan_block<false>(geo, wk, blockIdx.x, nblk, s_tmp, s_mx, &s_last)) fscan_final<false>(geo, wk, nblk, res, s_w, s_mx2, s_fl);
+    if (fscan_block(geo, wk, blockIdx.x, nblk, s_tmp, s_mx, &s_last)) fscan_final(geo, wk, nblk, res, s_w, s_mx2, s_fl);
 }
 
 // ---------------------------------------------------------------------------
 // k_emf: emission of tiles [t0, t1), one tile per wave.
 // ---------------------------------------------------------------------------
-__host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, uint32_t r) {
-    return ((ns << HH_FSM_ET_LG(K)) * 8u + (r ? (ns << r) * 8u : 0u) + ns * 8u + ns + 15u) & ~15u;
-}
 
 // The emission chain of one region (state, output dword, shift) while it
 // stores each step's symbols into the staging: every step's symbols are
@@ -1423,9 +941,7 @@ __host__ __device__ constexpr uint32_t emf_tab_bytes(uint32_t ns, uint32_t K, ui
 // when it is full (the last, partial one after the last step).  The unused
 // bytes of every stored dword are zero: a dword shared with the
 // neighbouring runs is repaired by OR afterwards (emf_edges).
-#ifndef HH_EMF_CPOL
-#define HH_EMF_CPOL 2         // k_emf's static copy-out stores: cache policy bits (2: nt -- 1 GiB kjv -3 % against plain)
-#endif
+#define EMF_CPOL 2            // k_emf's static copy-out stores: cache policy bits (2: nt -- 1 GiB kjv -3 % against plain)
 // Staging swizzle (SWZ, near-uniform codes): the dword at LDS byte address a
 // is kept at a ^ (((a >> 7) & 31) << 2), i.e. dwords are permuted within
 // each aligned 128-B chunk by the chunk's index.  Where every region emits
@@ -1455,15 +971,6 @@ __device__ __forceinline__ u32x4 emf_read16(const uint8_t *lds, uint32_t a) {
     return o;
 }
 
-#ifndef HH_XP_HEADS
-#define HH_XP_HEADS 0         // (timing experiments only)
-#endif
-#ifndef HH_XP_TRANS
-#define HH_XP_TRANS 0         // (timing experiments only)
-#endif
-#ifndef HH_EMF_PUT64
-#define HH_EMF_PUT64 1        // k_emf: a step's bytes shifted into the current dword with one 64-bit shift
-#endif
 template <uint32_t K, bool SWZ = false>
 struct EmfChain {
     uint32_t row, wd, sh, a;
@@ -1476,34 +983,18 @@ struct EmfChain {
     __device__ __forceinline__ uint32_t put(uint8_t *lds, uint64_t e) {
         const uint32_t lo = (uint32_t)e, hi = (uint32_t)(e >> 32);
         const uint32_t u = sh + (hi & 255u);          // 8 x the symbols: one SDWA add
-        if (HH_EMF_PUT64) {
-            // one 64-bit shift gives both the bytes that fit the current
-            // dword and those that spill into the next (none at sh = 0): 2
-            // VALU instead of 5 (shift-or, negate, alignbit, compare, select);
-            // the store through an LDS-space pointer (the staging's byte
-            // address is its LDS address: no base add)
-            const uint64_t t = (uint64_t)lo << sh;
-            const uint32_t an = (uint32_t)t | a;
-            const bool full = u >= 32;
-            if (full) *(lds_u32p)(uintptr_t)emf_swz<SWZ>(wd) = an;
-            a = full ? (uint32_t)(t >> 32) : an;
-            wd += full ? 4u : 0u;
-            sh = u & 31u;
-            return an;
-        }
-        // the bytes that do not fit the current dword spill into the next;
-        // K = 6 (and 5) steps carry at most 3 symbols, so nothing spills at
-        // sh = 0, K = 7 and K = 4 steps up to 4 (7 bits from inside a code:
-        // 1 + 3 x 2; 4 bits of 1-bit codes)
-        const uint32_t an = (lo << sh) | a;
-        uint32_t sp = __builtin_amdgcn_alignbit(0u, lo, (0u - sh) & 31u);
-        if (K != 6) sp = sh ? sp : 0u;
+        // one 64-bit shift gives both the bytes that fit the current dword
+        // and those that spill into the next (none at sh = 0): 2 VALU
+        // instead of 5 (shift-or, negate, alignbit, compare, select); the
+        // store through an LDS-space pointer (the staging's byte address is
+        // its LDS address: no base add).  A dword is stored once it is full
+        // (the run's last, partial one at the end): an exec-masked store's
+        // LDS cycles count its active lanes' addresses only.
+        const uint64_t t = (uint64_t)lo << sh;
+        const uint32_t an = (uint32_t)t | a;
         const bool full = u >= 32;
-        // the dword once it is full (the run's last, partial one at the end):
-        // an exec-masked store's LDS cycles count its active lanes' addresses
-        // only, and a dword fills every 2.5 steps on kjv
-        if (full) *(uint32_t *)(lds + emf_swz<SWZ>(wd)) = an;
-        a = full ? sp : an;
+        if (full) *(lds_u32p)(uintptr_t)emf_swz<SWZ>(wd) = an;
+        a = full ? (uint32_t)(t >> 32) : an;
         wd += full ? 4u : 0u;
         sh = u & 31u;
         return an;
@@ -1514,15 +1005,6 @@ struct EmfChain {
         row = HH_FSM_ET_ROW(e);
     }
 };
-#ifndef HH_EMF_PIPE
-#define HH_EMF_PIPE 1         // k_emf: step k+1's table read issued before step k's symbols are stored
-#endif
-#ifndef HH_SCAN_FUSED
-#define HH_SCAN_FUSED 0       // the tile scan inside the emission launch (k_emf), not a launch of its own
-#endif
-#ifndef HH_EMF_DYN
-#define HH_EMF_DYN 1          // k_emf: the workgroup's tiles claimed one at a time from an LDS counter
-#endif
 
 // NCH independent regions (one per chain: region j of NCH tiles) entered in
 // states s[c], their symbols to the staging from LDS byte address oa[c] on:
@@ -1548,7 +1030,7 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
 #pragma unroll
     for (uint32_t c = 0; c < NCH; c++) ch[c].init(s[c], oa[c]);
     constexpr uint32_t NST = S / K;
-    if (!TAIL && HH_EMF_PIPE) {
+    if (!TAIL) {
         // The chain's critical path is read -> next row -> next read; the
         // symbols' shifts, the full-dword test and the exec-masked store are
         // off it.  Step k+1's read (and after the last step the remainder
@@ -1557,18 +1039,6 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
         // overlaps the next read's latency (in program order the compiler
         // put the whole store block between a read's return and the next read).
         uint64_t e[NCH];
-#if HH_XP_HEADS
-        // (single-pass cost experiment: a head chain of HH_XP_HEADS steps from
-        // the root over the region's words before its emission, as a single
-        // pass would run per region; the result kept alive, not used)
-        {
-            uint32_t hh = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < HH_XP_HEADS; k++)
-                hh = (uint32_t)(*(const uint64_t __attribute__((address_space(3))) *)(uintptr_t)et_addr<SW, K>(hh, w[0], (k * K) % (S - K)) >> 32);
-            asm volatile("" :: "v"(hh));
-        }
-#endif
 #pragma unroll
         for (uint32_t c = 0; c < NCH; c++) e[c] = *(const uint64_t *)(lds + et_addr<SW, K>(ch[c].row, w[c], 0));
 #pragma unroll
@@ -1617,11 +1087,6 @@ __device__ __forceinline__ void emf_region(uint8_t *lds, uint32_t er_off, const 
     for (uint32_t c = 0; c < NCH; c++) {
         EmfChain<K, SWZ> &x = ch[c];
         if (!TAIL) {
-            if (r && !HH_EMF_PIPE) {
-                const uint64_t e = *(const uint64_t *)(lds + er_off + (x.row >> (HH_FSM_ET_LG(K) - r)) + (rbits<SW>(w[c], S - r, r) << 3));
-                x.put(lds, e);
-                x.row = HH_FSM_ET_ROW(e);
-            }
         } else {
             uint32_t st = x.row >> HH_FSM_ET_RSH(K);
             for (uint32_t q = lim / K * K; q < lim; q++) {
@@ -1673,14 +1138,14 @@ __device__ __forceinline__ void emf_direct(const uint32_t *b1, const uint8_t *ts
 // (vmcnt counts loads and stores in order) need not wait for this tile's
 // stores to reach memory.  With a data-dependent store loop it must: the
 // compiler waits vmcnt(0) at every tile's start (30 % of the kernel's wave
-// cycles in the HH_DIAG build).  (Round 3 measured a fixed COI of 16 no
+// cycles in round 3's cycle-stamp build).  (Round 3 measured a fixed COI of 16 no
 // faster: three quarters of its stores were empty.)
 // The emission of tiles [t0, t1) as workgroup blk of nblk (k_emf; and the
 // tail tiles run by k_emf's first workgroups).
 template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO, bool SWZ>
 __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const FsmGeo &geo, const FsmTab &tab,
                                         const FsmWork &wk, uint8_t *__restrict__ out, uint64_t cap, uint64_t t0,
-                                        uint64_t t1, uint32_t lds_bytes, uint32_t blk, uint32_t nblk, uint32_t epoch) {
+                                        uint64_t t1, uint32_t lds_bytes, uint32_t blk, uint32_t nblk) {
     static_assert(!TAIL || NCH == 1, "the tail tiles take one chain per lane");
     static_assert(!SWZ || !TAIL, "the tail tiles' staging is not swizzled");
     extern __shared__ __align__(16) uint8_t smem[];
@@ -1690,26 +1155,16 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     const uint32_t er_off = (ns << HH_FSM_ET_LG(K)) * 8u;
     uint32_t *s_b1 = (uint32_t *)(smem + er_off + (r ? (ns << r) * 8u : 0u));
     uint8_t *s_ts = (uint8_t *)(s_b1 + 2 * ns);
-    constexpr uint32_t EW = emf_waves(NCH);
-    WSPAN_START(0);
+    constexpr uint32_t EW = emf_waves();
     lds_fill16(smem, tab.et, (ns << HH_FSM_ET_LG(K)) * 8u);   // (ns x 2^LG u64: a multiple of 16 B)
     for (uint32_t i = tid; r && i < (ns << r); i += blockDim.x) ((uint64_t *)(smem + er_off))[i] = tab.er[i];
     for (uint32_t i = tid; i < 2 * ns; i += blockDim.x) s_b1[i] = tab.b1[i];
     for (uint32_t i = tid; i < ns; i += blockDim.x) s_ts[i] = tab.tsym[i];
     // the workgroup's tile counter (DYN), in the LDS's last 16 bytes
-    constexpr bool DYN = !TAIL && NCH == 1 && HH_EMF_DYN;
+    constexpr bool DYN = !TAIL && NCH == 1;
     const uint32_t ctr = lds_bytes - 16u;
     if (DYN && tid == 0) *(lds_u32p)(uintptr_t)ctr = 0u;
-    if (epoch && tid == 0) {
-        // HH_SCAN_FUSED: the scan's last block (k_emf's own workgroups, above)
-        // has published the bases (stored sc1)
-        while (__hip_atomic_load(&wk.flags[10], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) __builtin_amdgcn_s_sleep(1);
-    }
     __syncthreads();
-    // (then this CU's and XCD's caches invalidated, once: the bases, prefixes
-    // and the largest tile output are read with plain loads -- sc1 loads in
-    // the tile loop cost the emission 3 %)
-    if (epoch) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // staging per tile: the largest tile output + its 16-B misalignment + the
     // last step's overflow dword; the active waves share the rest of the LDS
     const uint32_t tabb = SWZ ? (emf_tab_bytes(ns, K, r) + 127u) & ~127u : emf_tab_bytes(ns, K, r);   // (SWZ: 128-B chunks)
@@ -1720,7 +1175,6 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     uint32_t nact = pool / (NCH * need);
     nact = nact > EW ? EW : nact < 1u ? 1u : nact;
     if (nact > blockDim.x / 64u) nact = blockDim.x / 64u;
-    WSPAN_FILLED();
     if (wv >= nact) return;                          // (no workgroup barrier after this point)
     const uint32_t obw = pool / (NCH * nact) & ~(SU - 1u);   // (>= need: need is a multiple of SU)
 
@@ -1737,10 +1191,7 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
             for (uint32_t c = 0; c < NCH; c++) {
                 uint64_t tt = tt0 + c * nwv;
                 tt = uni64(tt < t1 ? tt : tt0);
-#ifndef HH_XP_L2
-#define HH_XP_L2 0            // (timing experiments only: the first 64 tiles' words and records for every tile)
-#endif
-                const uint64_t tw = HH_XP_L2 ? (tt & 63u) : tt;
+                const uint64_t tw = tt;
                 const __amdgpu_buffer_rsrc_t rs = fs_rsrc(g, tw * TB / 32, geo.nwords);
                 prec[c] = wk.rec[tw * NR + j];
                 pfx[c] = wk.fx[tw * FX_W + (j & (FX_W - 1))];
@@ -1754,7 +1205,7 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
         // the order u = k nact + v, go to its waves one at a time from the
         // LDS counter -- with equal shares the workgroup's younger waves,
         // behind the older ones in the SIMDs' issue order, ended up to 25 %
-        // later (per-wave end times, HH_WSPAN build)
+        // later (round 5's per-wave end-time stamps)
         auto tile_of = [&](uint32_t u) -> uint64_t {
             const uint32_t k = u / nact;
             return t0 + (uint64_t)k * nwv + (uint64_t)blk * nact + (u - k * nact);
@@ -1765,7 +1216,6 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
             return tile_of((uint32_t)__builtin_amdgcn_readlane((int)u, 0));
         };
         uint64_t t = DYN ? claim() : t0 + (uint64_t)blk * nact + wv, tn = t;
-        EDIAG_DECL
         if (t < t1) prefetch(t);
         // (the first tile's loads complete here, once per wave: the compiler
         // orders them differently before the loop than inside it, and its
@@ -1819,32 +1269,12 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     #pragma unroll
             for (uint32_t x = 0; x < NCH; x++) tl[x] = live[x] && fit[x] && c[x] > 0 && L[x] + c[x] == Tout[x];
             WAVE_SYNC();                                  // the previous tiles' copy-out has read the staging
-            EDIAG_STAMP(0);
             emf_region<SW, K, TAIL, NCH, SWZ>(smem, er_off, s_b1, s_ts, w, ent, lim, at_end, oa, tl, lw, lwd, lpart);
             WAVE_SYNC();
-            EDIAG_STAMP(1);
     #pragma unroll
             for (uint32_t x = 0; x < NCH; x++)
                 if (live[x] && fit[x]) emf_edges<SWZ>(smem, lw[x], lwd[x], lpart[x]);
-#if HH_XP_TRANS
-            // (single-pass cost experiment: a lane-column transposition -- each
-            // lane reads HH_XP_TRANS dwords of its run and writes them back,
-            // as moving lane columns into a contiguous staging would)
             WAVE_SYNC();
-            {
-                const uint32_t b0 = oa[0] & ~3u, se = tabb + (wv * NCH + 1) * obw - 4u;   // (within the wave's slot)
-                uint32_t v[HH_XP_TRANS];
-#pragma unroll
-                for (uint32_t i = 0; i < HH_XP_TRANS; i++) v[i] = *(lds_u32p)(uintptr_t)min(b0 + 4 * i, se);
-                WAVE_SYNC();
-#pragma unroll
-                for (uint32_t i = 0; i < HH_XP_TRANS; i++) asm volatile("" : "+v"(v[i]));
-#pragma unroll
-                for (uint32_t i = 0; i < HH_XP_TRANS; i++) *(lds_u32p)(uintptr_t)min(b0 + 4 * i, se) = v[i];
-            }
-#endif
-            WAVE_SYNC();
-            EDIAG_STAMP(2);
     #pragma unroll
             for (uint32_t x = 0; x < NCH; x++) {
                 if (!(COI != 0) && !live[x]) continue;      // ((COI != 0): no branch around the stores; a dead tile's resource is empty)
@@ -1869,7 +1299,7 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
                             const uint32_t lo = 16 * (j + 64 * ii);
                             u32x4 v = {0u, 0u, 0u, 0u};
                             if (lo < end) v = emf_read16<SWZ>(smem, (uint32_t)(sb - smem) + lo);   // (LDS reads only where the tile has bytes)
-                            __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(lo >= a0[x] ? lo : 0x40000000u), 0, HH_EMF_CPOL);
+                            __builtin_amdgcn_raw_buffer_store_b128(v, ors, (int)(lo >= a0[x] ? lo : 0x40000000u), 0, EMF_CPOL);
                         }
                         __builtin_amdgcn_raw_buffer_store_b8(smem[emf_swz<SWZ>((uint32_t)(sb - smem) + q)], ors, (int)(pb ? q : 0x40000000u), 0, 0);
                     } else {
@@ -1892,7 +1322,6 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
                     emf_direct<SW>(s_b1, s_ts, w[x], ent[x], lim, at_end[x], out + P0[x] + L[x]);
                 }
             }
-            EDIAG_STAMP(3);
         }
     };
     // COI from this decode's largest tile output: the copy-out of a tile of
@@ -1902,57 +1331,21 @@ __device__ __forceinline__ void emf_run(const uint32_t *__restrict__ g, const Fs
     else if (!TAIL && SCO && per <= 8) tiles(std::integral_constant<uint32_t, 8>{});
     else if (!TAIL && SCO && per <= 16) tiles(std::integral_constant<uint32_t, 16>{});
     else tiles(std::integral_constant<uint32_t, 0>{});
-    EDIAG_FLUSH(wk.dbg);
-    if (!TAIL) WSPAN_END(wk.dbg, 8);
 }
 
 // k_emf: the emission of tiles [t0, t1); its first ntb workgroups (dispatched
 // first, resident beside the rest) emit the stream's last tiles [u0, u1)
 // with the stream-end checks (TAIL) -- a launch of their own after this one
 // cost a tile's time at the end of every decode.
-// HH_SCAN_FUSED (epoch != 0): the tile scan runs here, not in k_fscan1 --
-// the launch's workgroups claim its sblk blocks one at a time from a counter
-// (flags[11], never reset: every workgroup claims until a claim fails, so a
-// decode takes sblk + gridDim.x counts and the host passes this decode's
-// first, cbase), so that only workgroups already running do scan work and
-// none waits on one that has not started; the block that draws the last
-// ticket scans the block totals and publishes the bases sc1 with flags[10]
-// = epoch; then every workgroup fills its tables and waits for the flag.
-// The launch and the drain of k_fscan1 are gone.  (A compare-and-swap
-// counter tagged with the epoch instead: 257 workgroups contending for it
-// took 0.4 ms.)
 template <uint32_t SW, uint32_t K, bool TAIL, uint32_t NCH, bool SCO, bool SWZ = false>
-__global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
+__global__ __launch_bounds__(64 * emf_waves()) void k_emf(const uint32_t *__restrict__ g, FsmGeo geo, FsmTab tab, FsmWork wk,
                                                  uint8_t *__restrict__ out, uint64_t cap, uint64_t t0, uint64_t t1,
-                                                 uint32_t lds_bytes, uint64_t u0, uint64_t u1, uint32_t ntb, uint32_t sblk,
-                                                 uint32_t epoch, uint32_t cbase, uint32_t *res) {
-    if (epoch) {
-        static_assert(64 * emf_waves(NCH) == SCAN_TB || NCH != 1, "a scan block per workgroup");
-        extern __shared__ __align__(16) uint8_t smem[];
-        int32_t *s_tmp = (int32_t *)smem, *s_mx = s_tmp + 16, *s_mx2 = s_tmp + 32;
-        uint32_t *s_last = (uint32_t *)(s_tmp + 48), *s_fl = (uint32_t *)(s_tmp + 64);
-        uint32_t *s_b = (uint32_t *)(s_tmp + 80);
-        int64_t *s_w = (int64_t *)(smem + 512);
-        for (;;) {
-            if (threadIdx.x == 0) *s_b = __hip_atomic_fetch_add(&wk.flags[11], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - cbase;
-            __syncthreads();
-            const uint32_t b = *s_b;
-            __syncthreads();
-            if (b >= sblk) break;
-            if (fscan_block<true>(geo, wk, b, sblk, s_tmp, s_mx, s_last)) {
-                fscan_final<true>(geo, wk, sblk, res, s_w, s_mx2, s_fl);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-                if (threadIdx.x == 0) __hip_atomic_store(&wk.flags[10], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __syncthreads();
-        }
-    }
+                                                 uint32_t lds_bytes, uint64_t u0, uint64_t u1, uint32_t ntb) {
     if (!TAIL && blockIdx.x < ntb) {
-        emf_run<SW, K, true, 1, false, false>(g, geo, tab, wk, out, cap, u0, u1, lds_bytes, blockIdx.x, ntb, epoch);
+        emf_run<SW, K, true, 1, false, false>(g, geo, tab, wk, out, cap, u0, u1, lds_bytes, blockIdx.x, ntb);
         return;
     }
-    emf_run<SW, K, TAIL, NCH, SCO, SWZ>(g, geo, tab, wk, out, cap, t0, t1, lds_bytes, blockIdx.x - ntb, gridDim.x - ntb, epoch);
+    emf_run<SW, K, TAIL, NCH, SCO, SWZ>(g, geo, tab, wk, out, cap, t0, t1, lds_bytes, blockIdx.x - ntb, gridDim.x - ntb);
 }
 
 // ---------------------------------------------------------------------------
@@ -1961,7 +1354,7 @@ __global__ __launch_bounds__(64 * emf_waves(NCH)) void k_emf(const uint32_t *__r
 typedef void (*kcnt_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint64_t);
 typedef void (*kcntm_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint64_t, uint64_t, uint64_t, uint64_t, uint32_t);
 typedef void (*kemf_t)(const uint32_t *, FsmGeo, FsmTab, FsmWork, uint8_t *, uint64_t, uint64_t, uint64_t, uint32_t, uint64_t,
-                       uint64_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t *);
+                       uint64_t, uint32_t);
 
 #define FSM_SW_CASES(X) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12)
 // k_cntm for regions of S = 32 sw bits with count steps of cb bits (M =
@@ -1985,17 +1378,8 @@ static kcnt_t kcnt_for(uint32_t sw, bool tail, uint32_t cb) {
     default: return nullptr;
     }
 }
-// chains per lane of the main emission launch
-#ifndef HH_XP_EMF
-#define HH_XP_EMF 0           // (experiments: HH_EMF_NCH=2 chains per lane, HH_EMF_POOL staging bytes)
-#endif
-static uint32_t emf_nch() { return HH_XP_EMF && getenv("HH_EMF_NCH") ? (uint32_t)atoi(getenv("HH_EMF_NCH")) : 1u; }
 // (swz: the swizzled staging, with the static copy-out)
-static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sco, bool swz = false) {
-    (void)nch;   // (two chains per lane: measured slower, not instantiated)
-#if HH_XP_EMF
-    if (nch == 2 && !tail && sw == 8 && K == 7 && sco && !swz) return k_emf<8, 7, false, 2, true>;
-#endif
+static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, bool sco, bool swz = false) {
     switch (sw) {
 #define EMF_K(n, k)                                                                                       \
     (tail ? k_emf<n, k, true, 1, false> : swz ? k_emf<n, k, false, 1, true, true>                         \
@@ -2010,10 +1394,7 @@ static kemf_t kemf_for(uint32_t sw, uint32_t K, bool tail, uint32_t nch, bool sc
     }
 }
 
-#ifndef HH_XP_CNT_PAD
-#define HH_XP_CNT_PAD 0       // (occupancy experiments: LDS bytes added to the count launches')
-#endif
-static size_t lds_cnt(const FsmDev *fd) { return cnt_ctr_off(fd->ns, fd->cb) + 16u + HH_XP_CNT_PAD; }   // (+ k_cntm's chunk counter)
+static size_t lds_cnt(const FsmDev *fd) { return cnt_ctr_off(fd->ns, fd->cb) + 16u; }   // (+ k_cntm's chunk counter)
 // k_emf takes the whole LDS (one workgroup per CU) and sizes its stagings
 // from the largest tile output at run time
 #define EMF_LDS (160u * 1024u)
@@ -2094,12 +1475,12 @@ static int fsm_grids(FsmDev *fd) {
         return HH_OK;
     const uint32_t sw = fd->S / 32;
     const kcnt_t kc = kcnt_for(sw, false, fd->cb);
-    const kemf_t ke = kemf_for(sw, fd->K, false, emf_nch(), fd->sco, fd->swz);
+    const kemf_t ke = kemf_for(sw, fd->K, false, fd->sco, fd->swz);
     if (!kc || !ke) return HH_ERR_UNSUPPORTED;
     int pc = 0, pe = 0, ncu = 0, dev = 0;
     FS_OK(hipGetDevice(&dev));
     FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kc, 64 * CW, lds_cnt(fd)));
-    FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, ke, 64 * emf_waves(emf_nch()), lds_emf(fd)));
+    FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, ke, 64 * emf_waves(), lds_emf(fd)));
     FS_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     if (pc < 1 || pe < 1) return HH_ERR_UNSUPPORTED;
     fd->grid_c = (uint32_t)(pc * ncu);
@@ -2133,12 +1514,12 @@ static int ws_need(FsmWs *ws, size_t need) {
     if (hipMalloc(&ws->p, sz) != hipSuccess) return HH_ERR_NOMEM;
     ws->size = sz;
     FS_OK(hipMemset(ws->p, 0, 64));   // the status word and the scan's block ticket (the scan's last block clears it)
-    ws->cbase = 0;                     // (the fused scan's block counter, flags[11], starts again)
     return HH_OK;
 }
 
 void fsm_ws_free(FsmWs *ws) {
     if (ws->p) (void)hipFree(ws->p);
+    if (ws->st) (void)hipFree(ws->st);
     if (ws->h_res) (void)hipHostFree(ws->h_res);
     memset(ws, 0, sizeof(*ws));
 }
@@ -2158,8 +1539,18 @@ static int ws_side(FsmWs *ws) {
 // memory; *pd keeps what fsm_collect needs.
 int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void *d_data, uint64_t bits,
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap, hipStream_t st,
-               FsmPend *pd) {
+               FsmPend *pd, bool force_two) {
     if (!fd->ok) return HH_ERR_UNSUPPORTED;
+    // the single pass (hh_one.hip) unless the tree's tables leave it no room,
+    // the decoder asks for the two passes, or a single-pass decode of this
+    // stream handed it back
+    pd->nt_arg = ntiles;
+    pd->in_state = in_state;
+    if (fd->one_ok && !fd->two_pass && !fd->phases && !force_two) {
+        const int orc = one_launch(fd, ws, slot, ev, d_data, bits, ntiles, in_state, emit_from, d_out, cap, st, pd);
+        if (orc != HH_ERR_UNSUPPORTED) return orc;
+    }
+    pd->one = 0;
     if (slot >= FSM_RES_SLOTS) return HH_ERR_ARG;
     int rc = fsm_grids(fd);
     if (rc) return rc;
@@ -2196,15 +1587,8 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
     wk.fxs = (int32_t *)(w + o_fxs);
     wk.blk = (int64_t *)(w + o_blk);
     wk.bmax = (int32_t *)(w + o_bmax);
-    wk.dbg = fd->dbg;
     FsmTab tab = {fd->ct, fd->b1, fd->tsym, fd->et, fd->er};
     const uint32_t sw = fd->S / 32;
-#if defined(HH_DIAG)
-    if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, 16 * sizeof(uint64_t), st));
-#endif
-#if defined(HH_WSPAN)
-    if (wk.dbg) FS_OK(hipMemsetAsync(wk.dbg, 0, (16 + 10 * WSPAN_N) * sizeof(uint64_t), st));
-#endif
     rc = ws_side(ws);
     if (rc) return rc;
     FS_OK(hipEventRecord(ev[0], st));
@@ -2249,36 +1633,24 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
     // emission launch's first workgroups; a launch of their own without
     // tiles before them)
     const uint64_t ne = std::max<uint64_t>(emit_from, std::min<uint64_t>(bits / TB, nt));
-    // the scan inside the main emission launch (HH_SCAN_FUSED), else k_fscan1
-    const bool fused = HH_SCAN_FUSED && emit_from < nt && ne > emit_from && emf_nch() == 1 && nblk < 0xf000u &&
-                       !getenv("HH_NO_SCAN_FUSED");
-    uint32_t epoch = 0;
-    if (fused) {
-        if (++ws->epoch == 0) ws->epoch = 1;
-        epoch = ws->epoch;
-    } else {
-        hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk, nblk, ws->d_res + 16 * slot);
-        FS_OK(hipGetLastError());
-    }
+    hipLaunchKernelGGL(k_fscan1, dim3(nblk), dim3(SCAN_TB), 0, st, geo, wk, nblk, ws->d_res + 16 * slot);
+    FS_OK(hipGetLastError());
     if (fd->phases) FS_OK(hipEventRecord(ev[2], st));
     if (emit_from < nt) {
-        const uint32_t ew = emf_waves(emf_nch()), ew1 = emf_waves(1);
+        const uint32_t ew = emf_waves(), ew1 = emf_waves();
         const uint32_t ntb = (uint32_t)((nt - ne + ew1 - 1) / ew1);
         if (ne > emit_from) {
             const uint64_t nwg = (ne - emit_from + ew - 1) / ew;
             const uint32_t gm = fd->grid_e > ntb + 1 ? fd->grid_e - ntb : 1u;
             const uint32_t ge = (uint32_t)(nwg < gm ? nwg : gm) + ntb;
-            uint32_t ldsb = (uint32_t)lds_emf(fd);
-            if (HH_XP_EMF && getenv("HH_EMF_POOL")) ldsb = emf_tab_bytes(fd->ns, fd->K, fd->r) + (uint32_t)atoi(getenv("HH_EMF_POOL"));
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, false, emf_nch(), fd->sco, fd->swz), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, false, fd->sco, fd->swz), dim3(ge), dim3(64 * ew), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, emit_from, ne,
-                               ldsb, ne, nt, ntb, fused ? nblk : 0u, epoch, ws->cbase, ws->d_res + 16 * slot);
+                               (uint32_t)lds_emf(fd), ne, nt, ntb);
             FS_OK(hipGetLastError());
-            if (fused) ws->cbase += nblk + ge;   // (the counts this launch takes: see k_emf)
         } else if (ne < nt) {
-            hipLaunchKernelGGL(kemf_for(sw, fd->K, true, 1, false), dim3(ntb), dim3(64 * ew1), lds_emf(fd), st,
+            hipLaunchKernelGGL(kemf_for(sw, fd->K, true, false), dim3(ntb), dim3(64 * ew1), lds_emf(fd), st,
                                (const uint32_t *)d_data, geo, tab, wk, (uint8_t *)d_out, cap, ne, nt,
-                               (uint32_t)lds_emf(fd), (uint64_t)0, (uint64_t)0, 0u, 0u, 0u, 0u, (uint32_t *)nullptr);
+                               (uint32_t)lds_emf(fd), (uint64_t)0, (uint64_t)0, 0u);
             FS_OK(hipGetLastError());
         }
     }
@@ -2300,6 +1672,7 @@ int fsm_collect(FsmWs *ws, hipEvent_t *ev, const FsmPend *pd, uint64_t *total, u
     const uint64_t nt = pd->nt, emit_from = pd->emit_from, cap = pd->cap;
     const volatile uint32_t *res = ws->h_res + 16 * pd->slot;
     const uint32_t fl = res[0];
+    if (pd->one && (fl & ~(uint32_t)FF_FAIL)) return HH_ONE_RETRY;   // (the single pass handed it back)
     *total = (uint64_t)res[2] | ((uint64_t)res[3] << 32);
     *leave = res[4];
     *entry = res[5];
@@ -2324,7 +1697,13 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
                hipStream_t st, uint64_t *total, uint32_t *leave, uint32_t *entry, float *ms) {
     (void)h_flags;
     FsmPend pd;
-    const int rc = fsm_launch(fd, ws, 0, ev, d_data, bits, ntiles, in_state, emit_from, d_out, cap, st, &pd);
+    int rc = fsm_launch(fd, ws, 0, ev, d_data, bits, ntiles, in_state, emit_from, d_out, cap, st, &pd);
+    if (rc) return rc;
+    rc = fsm_collect(ws, ev, &pd, total, leave, entry, ms);
+    ws->last_one = pd.one;
+    if (rc != HH_ONE_RETRY) return rc;
+    ws->last_one = 0;
+    rc = fsm_launch(fd, ws, 0, ev, d_data, bits, ntiles, in_state, emit_from, d_out, cap, st, &pd, true);
     if (rc) return rc;
     return fsm_collect(ws, ev, &pd, total, leave, entry, ms);
 }

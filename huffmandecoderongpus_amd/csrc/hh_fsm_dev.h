@@ -29,6 +29,14 @@ struct FsmDev {
     uint64_t *dbg;           // HH_DIAG builds: phase cycles of k_cnt (16 x u64, the decoder's)
     uint32_t test_nosync;    // tests only (HH_TEST_NOSYNC=1 at set_tree): every decode reports chains
                              // that did not meet, so that the callers' exact fallbacks run
+    // the single-pass decode (hh_one.hip; one_setup): usable, head steps,
+    // column dwords per lane, waves per workgroup, LDS bytes, grid
+    uint32_t one_ok, one_gs, one_capd, one_nw, one_lds, one_grid;
+    uint32_t one_nbm;        // rounds of the workgroup's waves per claimed block
+    uint32_t one_dbg;        // counters of every decode into dbg (HH_ONE_DBG=1)
+    uint32_t one_test_retry; // tests only (HH_TEST_ONE_RETRY=1 at set_tree): every single-pass decode hands
+                             // itself back to the two passes, so that the callers' retries run
+    uint32_t two_pass;       // the two-pass pipeline only (HH_FLAG_TWO_PASS)
 };
 
 // One decode of tiles [0, ntiles) of the segment at d_data (bits readable
@@ -48,15 +56,23 @@ struct FsmWs {
     // decode.  FSM_RES_SLOTS slots of 16 words: a decode in flight and the
     // next one enqueued behind it (hh_decode_device_async) keep theirs apart.
     uint32_t *h_res, *d_res;
-    uint32_t epoch;           // the last decode's tag for the scan inside k_emf (HH_SCAN_FUSED)
-    uint32_t cbase;           // that scan's block counter (flags[11]) at the next decode's start
+    uint32_t epoch;           // the last single-pass decode's tag (hh_one.hip: its tile states)
+    uint64_t *st;             // the single pass's published tile words (+ its block counters), st_cap words
+    uint64_t st_cap;
+    uint32_t last_one;        // the last decode fsm_decode finished ran the single pass
 };
 #define FSM_RES_SLOTS 2
 // What fsm_collect needs of a decode fsm_launch enqueued.
 struct FsmPend {
     uint64_t nt, emit_from, cap;
     uint32_t slot, phases, test_nosync;
+    uint32_t one;             // the single pass (k_one) decoded
+    uint64_t nt_arg;          // the launch's ntiles and in_state arguments (a retry's)
+    uint32_t in_state;
 };
+// fsm_collect: the single pass handed the decode back (a wait that ran out,
+// more fix rounds than it allows): decode it again with the two passes
+#define HH_ONE_RETRY (-101)
 void fsm_ws_free(FsmWs *ws);
 int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const void *d_data, uint64_t bits,
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap,
@@ -66,12 +82,18 @@ int fsm_decode(FsmDev *fd, FsmWs *ws, uint32_t *h_flags, hipEvent_t *ev, const v
 // event and returns what fsm_decode would.
 int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void *d_data, uint64_t bits,
                uint64_t ntiles, uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap, hipStream_t st,
-               FsmPend *pd);
+               FsmPend *pd, bool force_two = false);
 int fsm_collect(FsmWs *ws, hipEvent_t *ev, const FsmPend *pd, uint64_t *total, uint32_t *leave, uint32_t *entry,
                 float *ms);
 int fsm_upload(FsmDev *fd, const hh_fsm_tables *F, uint32_t G, uint32_t minlen, uint32_t maxlen);
 bool fsm_k_fits(const hh_fsm_tables *F, uint32_t est_tile);   // F's emission tables leave room for 16 stagings
 void fsm_free(FsmDev *fd);
+// the single pass (hh_one.hip): its geometry for the tables in fd (G: head
+// bits, avg: expected bits per symbol), and the launch half (fsm_launch's
+// contract; fsm_launch calls it unless fd->two_pass or force_two)
+void one_setup(FsmDev *fd, uint32_t G, double avg, uint32_t minlen);
+int one_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void *d_data, uint64_t bits, uint64_t ntiles,
+               uint32_t in_state, uint64_t emit_from, void *d_out, uint64_t cap, hipStream_t st, FsmPend *pd);
 int fsm_debug_arrays(const FsmWs *ws, uint64_t nt, uint32_t *rec, uint32_t *fx, int32_t *tsum, uint32_t *xs);
 
 #endif

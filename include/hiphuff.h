@@ -172,6 +172,12 @@ typedef struct {
                                    decodes the same buffers again and again,
                                    as the reference's evaluate() does
                                    (decodeUtil.c:41-43, 54-68). */
+#define HH_FLAG_TWO_PASS 64     /* the state-machine decode in its two-pass
+                                   form (k_cntm count pass, k_fscan1 scan,
+                                   k_emf emission) instead of the single pass
+                                   (k_one: speculative emission, decoupled
+                                   look-back); HH_FLAG_PHASE_TIMING implies
+                                   it (the split is between its kernels) */
 
 int hh_decoder_create(hh_decoder **dec, const hh_config *cfg);
 void hh_decoder_destroy(hh_decoder *dec);
@@ -197,8 +203,9 @@ typedef struct {
                                 that does not resynchronise)                */
     int fixed_length;        /* 1: a complete fixed-length code, unpacked
                                 by k_fixed (HH_FLAG_NO_FIXED: 0)            */
-    int state_machine;       /* 1: the state-machine decode ran (k_cnt,
-                                k_fscan, k_emf)                             */
+    int state_machine;       /* the state-machine decode ran: 1 its two
+                                passes (k_cntm, k_fscan1, k_emf), 2 its
+                                single pass (k_one)                         */
 } hh_stats;
 
 int hh_decoder_stats(const hh_decoder *dec, hh_stats *st);
