@@ -59,6 +59,10 @@ def _args():
                     help="skip the E.coli / i.i.d. workloads and the evaluate()-scope timing")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_latest.json"),
                     help="HBM traffic measured by rocprofv3 --pmc (tools/profile.sh)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (nccl = RCCL; gloo: tests)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on cuda:0 (tests of the N > 1 path on a one-GPU box; gloo only)")
     return ap.parse_args()
 
 
@@ -390,7 +394,7 @@ def launch_ranks(a) -> int:
     import subprocess
     import torch
     have = torch.cuda.device_count()
-    if have < a.gpus:
+    if have < a.gpus and not a.one_device:
         raise SystemExit(f"bench.py --gpus {a.gpus}: only {have} GPU(s) visible on this node")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={a.gpus}", "--master-addr", "127.0.0.1",
@@ -415,9 +419,13 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.one_device:
+        if a.backend != "gloo":
+            raise SystemExit("bench.py --one-device needs --backend gloo (RCCL refuses two ranks on one GPU)")
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(a.backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -458,12 +466,12 @@ def main():
 
     for _ in range(a.warmup):
         if world > 1:
-            job.decode_step()               # (the timed form: queued, no exchange)
+            job.full_step()                 # (the timed form: decode, exchange, any redo)
         else:
             run_step()
-    if world > 1:
-        job.wait()
     torch.cuda.synchronize()
+    # (collectives over host tensors with gloo)
+    red_dev = torch.device("cpu") if world > 1 and a.backend == "gloo" else dev
     sync_ms = None
     if world == 1:
         # the synchronous call (hh_decode_device: returns once the length is
@@ -489,17 +497,16 @@ def main():
         dec.wait()
         dev_ms.append(dec.stats())
     else:
-        # the rank's shard decodes only (the prologue decode, and the redo
-        # from the settled entry if the checked step needed one), queued
-        # asynchronously: no collective and no host wait inside the timed
-        # steps -- the entry exchange ran on the checked step above and runs
-        # once more after the timed region (job.confirm)
+        # a full step per rank: its shard's decode (prologue + owned tiles,
+        # entered in the guessed state), the entry exchange (5 integers,
+        # all-gather: it proves every entry and gives the output bases) and
+        # the redo of a wrong entry -- nothing carried over from the checked
+        # step; every step's rows must equal the checked step's
+        steps_ok = True
         for k in range(a.steps):
-            job.decode_step()
-            if k:
-                dev_ms.append(dec.stats())      # (the decode checked by this call)
-        job.wait()
-        dev_ms.append(dec.stats())
+            job.full_step()
+            dev_ms.append(dec.stats())
+            steps_ok = steps_ok and job.last_rows == job.rows
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -508,7 +515,7 @@ def main():
     if world == 1 and any(int(n.value) != syn.decoded_bytes for n in lens):
         raise SystemExit("a timed decode returned the wrong length")
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -522,16 +529,33 @@ def main():
                else "k_front+k_walk+k_table+k_scan1+k_scan2+k_emit")
     extra = {}
     if world > 1:
-        confirmed = torch.tensor([1 if job.confirm() else 0], dtype=torch.int64, device=dev)
+        # the decode alone (the figure for the decode-time scaling target):
+        # each rank's shard decodes queued asynchronously, entered in the
+        # settled entry -- no exchange inside; the exchange over the last
+        # one's results after the region must reproduce the checked rows
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(a.steps):
+            job.decode_step()
+        job.wait()
+        torch.cuda.synchronize()
+        dist.barrier()
+        td = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(td, op=dist.ReduceOp.MAX)
+        confirmed = torch.tensor([1 if (job.confirm() and steps_ok) else 0], dtype=torch.int64, device=red_dev)
         dist.all_reduce(confirmed, op=dist.ReduceOp.MIN)
         extra = job.gather_report()
-        extra["settle"] = {"redo_in_timed_steps": job.redo_state is not None,
+        ms_dec = float(td.item()) / a.steps * 1e3
+        extra["settle"] = {"timed_step": "decode + 5-integer entry all-gather + any redo (job.full_step)",
+                           "redo_on_checked_step": job.redo_state is not None,
                            "confirmed_after_timed": bool(confirmed.item()),
-                           "exchange": "5-integer all-gather on the checked step and once after the timed "
-                                       "steps; none inside them"}
+                           "decode_only": {"ms_per_step": round(ms_dec, 4),
+                                           "note": "shard decodes alone, entered in the settled entry, "
+                                                   "queued asynchronously; the exchange after them"}}
         if not confirmed.item():
-            raise SystemExit(f"rank {rank}: the entry exchange after the timed steps disagrees")
-        tot = torch.tensor([C_bytes, D_bytes], dtype=torch.float64, device=dev)
+            raise SystemExit(f"rank {rank}: the entry exchange of a timed step disagrees with the checked one")
+        tot = torch.tensor([C_bytes, D_bytes], dtype=torch.float64, device=red_dev)
         dist.all_reduce(tot)
         C_all, D_all = int(tot[0].item()), int(tot[1].item())
     else:

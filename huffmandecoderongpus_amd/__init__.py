@@ -100,6 +100,10 @@ _SIGS = {
                    C.POINTER(C.c_uint64)], C.c_int),
     "hh_encode_device": ([C.POINTER(_Tree), C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                           C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
+    "hh_encoder_create": ([C.POINTER(C.c_void_p), C.c_int], C.c_int),
+    "hh_encoder_destroy": ([C.c_void_p], None),
+    "hh_encoder_encode": ([C.c_void_p, C.POINTER(_Tree), C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                           C.POINTER(C.c_uint64), C.c_void_p], C.c_int),
     "hh_decoder_create": ([C.POINTER(C.c_void_p), C.POINTER(_Config)], C.c_int),
     "hh_decoder_destroy": ([C.c_void_p], None),
     "hh_decoder_set_tree": ([C.c_void_p, C.POINTER(_Tree)], C.c_int),
@@ -152,12 +156,21 @@ def lib() -> C.CDLL:
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
         L = C.CDLL(LIB_PATH)
+        # every declared symbol must be there; only an explicit A/B build
+        # of an older revision (HIPHUFF_AB_BUILD=1, tools/mkrev.sh) may lack
+        # some -- those are named on stderr and left unbound
+        ab = os.environ.get("HIPHUFF_AB_BUILD") == "1"
+        skipped = []
         for name, (args, res) in _SIGS.items():
-            if (name.startswith("hh_debug_") or os.environ.get("HIPHUFF_LIB")) and not hasattr(L, name):
-                continue                              # (diagnostics; older A/B builds lack them)
+            if ab and not hasattr(L, name):
+                skipped.append(name)
+                continue
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res
+        if skipped:
+            import sys
+            print(f"hiphuff: {LIB_PATH} (HIPHUFF_AB_BUILD) lacks {', '.join(skipped)}", file=sys.stderr)
         _lib_handle = L
     return _lib_handle
 
@@ -258,6 +271,36 @@ def encode_device(tree: "Tree", syms, out, stream=None) -> int:
     return int(bits.value)
 
 
+class Encoder:
+    """A device encoder (hh_encoder_*): its own workspace, so that encoders
+    on different streams (or threads) encode at once."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        _check(lib().hh_encoder_create(C.byref(self._h), device), "encoder create")
+
+    def encode(self, tree: "Tree", syms, out, stream=None) -> int:
+        """encode_device on this encoder."""
+        import torch
+        assert syms.is_cuda and out.is_cuda and syms.dtype == torch.uint8 and out.dtype == torch.uint8
+        bits = C.c_uint64(0)
+        _check(lib().hh_encoder_encode(self._h, C.byref(tree._c), syms.data_ptr(), syms.numel(), out.data_ptr(),
+                                       out.numel(), C.byref(bits), stream.cuda_stream if stream is not None else None),
+               "encoder_encode")
+        return int(bits.value)
+
+    def close(self):
+        if self._h:
+            lib().hh_encoder_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def copy_device(src, dst, nt: bool = False, stream=None) -> float:
     """hh_copy_device on torch uint8 CUDA tensors (the same number of bytes,
     a multiple of 16): the streaming-copy reference; returns its device ms."""
@@ -291,14 +334,17 @@ class Decoder:
         cfg = _Config(device, lane_bits, flags)
         _check(lib().hh_decoder_create(C.byref(self._h), C.byref(cfg)), "decoder create")
         self.device = device
+        self.flags = flags
         self._tree = None
         self._pending = []          # buffers of asynchronous decodes, kept alive until wait()
+        self._pinned = None         # (payload, out) FLAG_KEEP_HOST_PINNED keeps registered
 
     def close(self):
         if self._h:
             lib().hh_decoder_destroy(self._h)   # (waits for an asynchronous decode still running)
             self._h = C.c_void_p()
         self._pending = []
+        self._pinned = None
 
     def __del__(self):
         try:
@@ -320,18 +366,29 @@ class Decoder:
         """The evaluate() scope: host payload in, host symbols out.  `out`
         (uint8, >= cap) may be the caller's buffer, allocated and touched
         beforehand as evaluate() does (decodeUtil.c:37-38, 55)."""
+        keep = bool(self.flags & FLAG_KEEP_HOST_PINNED)
+        given = payload
         payload = np.ascontiguousarray(payload, np.uint8)
+        if keep and (out is None or payload is not given):
+            # the decoder keeps both buffers registered after the call: they
+            # must be the caller's own arrays, alive until release_host()
+            # (a temporary freed after the call could be reallocated at the
+            # same address and pass for the registered one)
+            raise ValueError("FLAG_KEEP_HOST_PINNED: pass a contiguous uint8 payload and an `out` buffer")
         if out is None:
             out = np.zeros(max(cap, 1), np.uint8)
         assert out.dtype == np.uint8 and out.flags.c_contiguous and out.size >= cap
         n = C.c_uint64(0)
         _check(lib().hh_decode_host(self._h, payload.ctypes.data, bits, out.ctypes.data, cap,
                                     C.byref(n)), "decode_host")
+        if keep:
+            self._pinned = (payload, out)     # (alive while registered)
         return out[: n.value]
 
     def release_host(self) -> None:
         """hh_decoder_release_host: unpin the buffers FLAG_KEEP_HOST_PINNED kept."""
         _check(lib().hh_decoder_release_host(self._h), "release_host")
+        self._pinned = None
 
     def decode_device_ptr(self, d_data: int, bits: int, d_out: int, cap: int,
                           stream: int = 0) -> int:

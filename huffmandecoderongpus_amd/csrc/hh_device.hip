@@ -1432,6 +1432,8 @@ struct hh_decoder {
     // caller buffers kept page-locked across calls (HH_FLAG_KEEP_HOST_PINNED)
     const void *pin_p[2];
     size_t pin_n[2];
+    int pin_own[2];      // 1: pin_p[k] registered for buffer k (pages pin_ra..pin_rb); 0: inside k^1's
+    uintptr_t pin_ra[2], pin_rb[2];
     // the asynchronous decode not checked yet (hh_decode_device_async)
     struct {
         int active;
@@ -2428,28 +2430,54 @@ static uint64_t pipe_chunk() {
 
 // HH_FLAG_KEEP_HOST_PINNED: buffer k (0 payload, 1 output) page-locked
 // from p for at least n bytes, the registration kept for later calls
-static int pin_host(hh_decoder *d, int k, const void *p, size_t n) {
-    if (d->pin_p[k] == p && d->pin_n[k] >= n) return HH_OK;
-    if (d->pin_p[k]) (void)hipHostUnregister((void *)d->pin_p[k]);
+// from p for at least n bytes, the registration kept for later calls.
+// Registrations are whole pages and may not overlap: a buffer whose pages
+// lie inside the other buffer's registration is recorded as covered by it
+// (pin_own 0), one that overlaps it partly gets a registration of the union
+// of both (the other then covered by it); when a registration goes, the
+// buffer it covered is pinned again.
+static bool pin_inside(const hh_decoder *d, int k, uintptr_t a, uintptr_t b) {
+    return d->pin_p[k] && d->pin_own[k] && a >= d->pin_ra[k] && b <= d->pin_rb[k];
+}
+static void pin_drop(hh_decoder *d, int k) {
+    if (d->pin_p[k] && d->pin_own[k]) (void)hipHostUnregister((void *)d->pin_ra[k]);
     d->pin_p[k] = nullptr;
     d->pin_n[k] = 0;
-    // (the other buffer may be the same memory: then it is registered already)
-    if (d->pin_p[k ^ 1] && (const uint8_t *)p >= (const uint8_t *)d->pin_p[k ^ 1] &&
-        (const uint8_t *)p + n <= (const uint8_t *)d->pin_p[k ^ 1] + d->pin_n[k ^ 1])
+    d->pin_own[k] = 0;
+    d->pin_ra[k] = d->pin_rb[k] = 0;
+}
+static int pin_host(hh_decoder *d, int k, const void *p, size_t n) {
+    uintptr_t a = (uintptr_t)p & ~(uintptr_t)4095, b = ((uintptr_t)p + n + 4095) & ~(uintptr_t)4095;
+    if (d->pin_p[k] == p && d->pin_n[k] >= n && (d->pin_own[k] || pin_inside(d, k ^ 1, a, b))) return HH_OK;
+    const int o = k ^ 1;
+    const void *op = d->pin_p[o];
+    const size_t on = d->pin_n[o];
+    bool repin = op && !d->pin_own[o];               // (o relied on k's registration)
+    pin_drop(d, k);
+    if (pin_inside(d, o, a, b)) {                     // (within the other buffer's pages)
+        d->pin_p[k] = p;
+        d->pin_n[k] = n;
         return HH_OK;
-    if (hipHostRegister((void *)p, n, hipHostRegisterDefault) != hipSuccess) return HH_ERR_UNSUPPORTED;
+    }
+    if (op && d->pin_own[o] && a < d->pin_rb[o] && d->pin_ra[o] < b) {
+        // a partial overlap: one registration of both
+        a = std::min(a, d->pin_ra[o]);
+        b = std::max(b, d->pin_rb[o]);
+        pin_drop(d, o);
+        repin = true;
+    }
+    if (hipHostRegister((void *)a, b - a, hipHostRegisterDefault) != hipSuccess) return HH_ERR_UNSUPPORTED;
     d->pin_p[k] = p;
     d->pin_n[k] = n;
-    return HH_OK;
+    d->pin_own[k] = 1;
+    d->pin_ra[k] = a;
+    d->pin_rb[k] = b;
+    return repin ? pin_host(d, o, op, on) : HH_OK;
 }
 
 extern "C" int hh_decoder_release_host(hh_decoder *d) {
     if (!d) return HH_ERR_ARG;
-    for (int k = 0; k < 2; k++) {
-        if (d->pin_p[k]) (void)hipHostUnregister((void *)d->pin_p[k]);
-        d->pin_p[k] = nullptr;
-        d->pin_n[k] = 0;
-    }
+    for (int k = 0; k < 2; k++) pin_drop(d, k);
     return HH_OK;
 }
 

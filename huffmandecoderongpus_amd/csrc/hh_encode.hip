@@ -17,6 +17,7 @@
 // HBM-bound: 1 B read per symbol, its code bits written once.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <mutex>
 
@@ -179,9 +180,41 @@ __global__ __launch_bounds__(ENC_TB) void k_enc_pack(const uint8_t *__restrict__
     }
 }
 
-extern "C" int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_t n, void *d_out, uint64_t cap,
-                                uint64_t *bits, void *hip_stream) {
-    if (!tree || !bits || (!d_syms && n) || (!d_out && cap)) return HH_ERR_ARG;
+// An encoder: the workspace of one device's encodes (the table, the chunks'
+// bits / offsets, the total and the absent-symbol flag), kept across calls
+// and grown when a call needs more.  Calls on one encoder run one at a time
+// (each returns when its encode is done); encoders are independent, so
+// encodes on several streams run at once with one encoder each.
+struct hh_encoder {
+    int device;
+    uint8_t *ws;
+    size_t size;
+};
+
+extern "C" int hh_encoder_create(hh_encoder **enc, int device) {
+    if (!enc) return HH_ERR_ARG;
+    *enc = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return HH_ERR_ARG;
+    hh_encoder *e = (hh_encoder *)calloc(1, sizeof(hh_encoder));
+    if (!e) return HH_ERR_NOMEM;
+    e->device = device;
+    *enc = e;
+    return HH_OK;
+}
+
+extern "C" void hh_encoder_destroy(hh_encoder *enc) {
+    if (!enc) return;
+    if (enc->ws) {
+        (void)hipSetDevice(enc->device);
+        (void)hipFree(enc->ws);                        // (every encode on it has returned: nothing in flight)
+    }
+    free(enc);
+}
+
+extern "C" int hh_encoder_encode(hh_encoder *enc, const hh_tree *tree, const void *d_syms, uint64_t n, void *d_out,
+                                 uint64_t cap, uint64_t *bits, void *hip_stream) {
+    if (!enc || !tree || !bits || (!d_syms && n) || (!d_out && cap)) return HH_ERR_ARG;
     if (((uintptr_t)d_out & 3u) != 0) return HH_ERR_ARG;   // (32-bit word stores)
     *bits = 0;
     EncTab h;
@@ -190,33 +223,23 @@ extern "C" int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_
     if (rc) return rc;
     for (int i = 0; i < 256; i++) h.len[i] = len8[i];
     if (n == 0) return HH_OK;
+    if (hipSetDevice(enc->device) != hipSuccess) return HH_ERR_DEVICE;
     hipStream_t st = (hipStream_t)hip_stream;
     const uint64_t nch = (n + ENC_CH - 1) / ENC_CH;
     // (a launch's grid may not exceed 2^32 - 1 threads: about 2^24 chunks,
     // 68.7 G symbols, with ENC_TB threads each)
     if (nch * ENC_TB > 0xffffffffull) return HH_ERR_UNSUPPORTED;
-    // workspace: the table, the chunks' bits / offsets, the total and the
-    // absent-symbol flag -- kept across calls per device (grown when a call
-    // needs more; one call at a time per process: a per-call allocation and
-    // free cost more than the kernels at 64 MiB)
     const size_t o_cb = (sizeof(EncTab) + 255) & ~(size_t)255, o_res = o_cb + ((nch * 8 + 255) & ~(size_t)255);
-    static std::mutex mu;
-    static uint8_t *s_ws[64];
-    static size_t s_sz[64];
-    std::lock_guard<std::mutex> lock(mu);
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return HH_ERR_DEVICE;
-    if (s_sz[dev] < o_res + 64) {
-        if (s_ws[dev]) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(s_ws[dev]);
-            s_ws[dev] = nullptr;
-            s_sz[dev] = 0;
-        }
-        if (hipMalloc(&s_ws[dev], o_res + 64) != hipSuccess) return HH_ERR_NOMEM;
-        s_sz[dev] = o_res + 64;
+    if (enc->size < o_res + 64) {
+        // (the previous encode on this encoder has returned: its stream is
+        // done with the old workspace, no device-wide wait)
+        if (enc->ws) (void)hipFree(enc->ws);
+        enc->ws = nullptr;
+        enc->size = 0;
+        if (hipMalloc(&enc->ws, o_res + 64) != hipSuccess) return HH_ERR_NOMEM;
+        enc->size = o_res + 64;
     }
-    uint8_t *ws = s_ws[dev];
+    uint8_t *ws = enc->ws;
     EncTab *d_tab = (EncTab *)ws;
     uint64_t *d_cb = (uint64_t *)(ws + o_cb), *d_res = (uint64_t *)(ws + o_res);
     uint32_t *d_bad = (uint32_t *)(ws + o_res + 32);
@@ -245,4 +268,20 @@ extern "C" int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_
         rc = HH_OK;
     } while (0);
     return rc;
+}
+
+// The handle-free form: one encoder per device for the process, calls
+// serialised on it.
+extern "C" int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_t n, void *d_out, uint64_t cap,
+                                uint64_t *bits, void *hip_stream) {
+    static std::mutex mu;
+    static hh_encoder *s_enc[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return HH_ERR_DEVICE;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!s_enc[dev]) {
+        const int rc = hh_encoder_create(&s_enc[dev], dev);
+        if (rc) return rc;
+    }
+    return hh_encoder_encode(s_enc[dev], tree, d_syms, n, d_out, cap, bits, hip_stream);
 }

@@ -16,14 +16,16 @@ state and lets a rank entered wrongly decode again with the right one (in
 at most world-1 more rounds; never needed when the prologue was exact), and
 (b) gives every rank its output base (exclusive sum of symbol counts).
 
-The exchange runs on a CHECKED step (check_step, before the timed region);
-the timed steps (decode_step) are the rank's decodes alone -- the prologue
-decode, plus the redo from the settled entry when the checked step needed
-one -- queued asynchronously, with no collective and no host wait; after
-the timed region one more exchange over the last timed step's results
-(confirm) must reproduce the checked step's rows.  The data path therefore
-has no collective; assembling the global output is one all-gather of the
-decoded segments, timed separately (bench.py gather_report).
+Every step bench.py times is a full step (full_step): the decode, the
+exchange and any redo, nothing carried over from an earlier step; its rows
+must reproduce those of the CHECKED step before the timed region
+(check_step).  bench.py also times the decodes alone (decode_step: the
+prologue decode, plus the redo from the settled entry when the checked step
+needed one, queued asynchronously with no collective; the exchange over
+the last one's results afterwards, confirm, must reproduce the checked
+rows) and reports them apart, as the decode-time figure.  Assembling the
+global output is one all-gather of the decoded segments, timed separately
+(bench.py gather_report).
 
 The settle protocol is pure Python over a `gather` callable so that it is
 tested with gloo on CPU (tests/test_shard.py) against the kernel's host
@@ -214,6 +216,7 @@ class ShardJob:
         self.decoded_bytes = 0
         self.rows = None
         self.redo_state = None
+        self.last_rows = self.last_redo = None
         self._last = None
         self._dist = dist
         # tests: a rank without a prologue enters in a state known to be
@@ -263,17 +266,25 @@ class ShardJob:
             r["entry_exact"] = False          # no prologue: the entry is a guess
         return r
 
-    def check_step(self) -> int:
-        """The checked decode of this rank's shard (before the timed region):
-        the decode, the entry-state exchange (settle), the redo of a wrong
-        entry.  Fixes what the timed steps decode."""
+    def full_step(self) -> int:
+        """One complete decode of this rank's shard: the decode entered in
+        the guessed state (prologue + owned tiles), the entry-state exchange
+        (settle: a 5-integer all-gather that proves every entry and gives the
+        output bases), the redo of a wrong entry.  Nothing is carried over
+        from an earlier step.  Collective (every rank calls it)."""
         s = self.seg
         first = self._first(self._decode(self.guess, s.prologue))
-        res, rows, self.redo_state = check_settle(first, lambda st: self._decode(st, 0), self._gather,
-                                                  self.rank, self.world)
-        self.rows = rows
-        self.decoded_bytes = res["out_len"]
+        res, rows, redo = check_settle(first, lambda st: self._decode(st, 0), self._gather, self.rank, self.world)
+        self.last_rows, self.last_redo = rows, redo
         return res["out_len"]
+
+    def check_step(self) -> int:
+        """The checked decode of this rank's shard (before the timed region):
+        a full step whose rows every later step must reproduce."""
+        n = self.full_step()
+        self.rows, self.redo_state = self.last_rows, self.last_redo
+        self.decoded_bytes = n
+        return n
 
     def decode_step(self) -> None:
         """One timed decode of this rank's shard: the prologue decode and, when

@@ -113,15 +113,22 @@ hh_tree hh_huff_tree(const hh_huff *h);
 uint64_t hh_encode_bound(const hh_tree *tree, uint64_t n);
 int hh_encode(const hh_tree *tree, const uint8_t *syms, uint64_t n,
               uint8_t *out, uint64_t *bits);
-/* The same on the GPU: n symbols at device pointer d_syms packed into
- * device buffer d_out (cap bytes, 4-byte aligned; it must hold the stream
- * rounded up to whole 32-bit words -- hh_encode_bound always does).  The
- * same bytes as hh_encode.  *bits gets the length (also with
- * HH_ERR_CAPACITY).  Enqueued on hip_stream; returns when done.  Calls are
- * serialised process-wide (one workspace per device, the current device's,
- * kept across calls and grown with a device synchronisation): encodes from
- * several threads or streams run one after another.  At most about 2^36
- * symbols per call (HH_ERR_UNSUPPORTED beyond: the launch's grid limit). */
+/* The same on the GPU through an encoder (its device's workspace, kept
+ * across calls): n symbols at device pointer d_syms packed into device
+ * buffer d_out (cap bytes, 4-byte aligned; it must hold the stream rounded
+ * up to whole 32-bit words -- hh_encode_bound always does).  The same bytes
+ * as hh_encode.  *bits gets the length (also with HH_ERR_CAPACITY).
+ * Enqueued on hip_stream; returns when done.  One call at a time per
+ * encoder; encoders are independent (one per stream encodes at once).  At
+ * most about 2^36 symbols per call (HH_ERR_UNSUPPORTED beyond: the launch's
+ * grid limit). */
+typedef struct hh_encoder hh_encoder;
+int hh_encoder_create(hh_encoder **enc, int device);
+void hh_encoder_destroy(hh_encoder *enc);
+int hh_encoder_encode(hh_encoder *enc, const hh_tree *tree, const void *d_syms, uint64_t n,
+                      void *d_out, uint64_t cap, uint64_t *bits, void *hip_stream);
+/* hh_encoder_encode on a process-wide encoder of the current device (calls
+ * serialised on it). */
 int hh_encode_device(const hh_tree *tree, const void *d_syms, uint64_t n,
                      void *d_out, uint64_t cap, uint64_t *bits, void *hip_stream);
 

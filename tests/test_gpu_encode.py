@@ -128,3 +128,47 @@ def test_encode_device_errors(hh):
     with pytest.raises(hh.HipHuffError):
         hh.encode_device(tree, d, out[:8])
     assert hh.encode_device(tree, d[:0], out) == 0
+
+
+def test_two_encoders_two_streams(hh):
+    """Encoders with their own workspaces (hh_encoder_*):
+    two threads, each with an encoder and a stream, encode different trees'
+    streams at once -- repeatedly, with growing sizes (workspace growth
+    without a device-wide wait) -- each byte-identical to the host encoder."""
+    import threading
+    import torch
+    rng = np.random.default_rng(123)
+    jobs = []
+    for k, nleaves in enumerate((40, 200)):
+        iz, io, sy, syms = _random_tree(rng, nleaves)
+        tree = hh.Tree(iz, io, sy)
+        text = rng.choice(syms, size=3_000_000 + 77777 * k).astype(np.uint8)
+        jobs.append((tree, text))
+    errs = []
+
+    def work(k):
+        try:
+            tree, text = jobs[k]
+            enc = hh.Encoder(0)
+            st = torch.cuda.Stream()
+            for n in (100_000, 1_000_003, text.size):
+                ref, rbits = tree.encode(text[:n])
+                d_syms = torch.from_numpy(text[:n]).cuda()
+                cap = (rbits + 31) // 32 * 4 + 64
+                out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+                torch.cuda.synchronize()
+                bits = enc.encode(tree, d_syms, out, st)
+                st.synchronize()
+                got = out[: (bits + 7) // 8].cpu().numpy()
+                if bits != rbits or not np.array_equal(got, ref[: (rbits + 7) // 8]):
+                    errs.append((k, n, bits, rbits))
+            enc.close()
+        except Exception as e:                        # (reported by the main thread)
+            errs.append((k, repr(e)))
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs

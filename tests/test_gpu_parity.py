@@ -354,6 +354,46 @@ def test_evaluate_scope_keeps_buffers_pinned(hh, files_dir, monkeypatch):
         dec.close()
 
 
+def test_kept_pins_follow_the_buffers(hh, files_dir):
+    """HH_FLAG_KEEP_HOST_PINNED with buffers that share memory:
+    a payload lying inside the output buffer's registration, then a new
+    output buffer (the payload must be pinned on its own again), then a
+    payload that overlaps the output's registration without being inside it
+    -- every call decodes right; and the Python binding refuses the flag
+    with a temporary output or a copied payload (freed after the call, their
+    address could pass for a registered buffer)."""
+    path = os.path.join(files_dir, "paper1.huff")
+    hf = hh.HuffFile.load(path)
+    ref = O.OracleHuff.load(path).chain_decode()
+    nb, n = (hf.bits + 7) // 8, hf.uncompressedsize
+    dec = hh.Decoder(0, flags=hh.FLAG_KEEP_HOST_PINNED)
+    try:
+        dec.set_tree(hf.tree())
+        with pytest.raises(ValueError):
+            dec.decode_host(hf.payload, hf.bits, n + 16)                 # (no out)
+        with pytest.raises(ValueError):
+            dec.decode_host(hf.payload.astype(np.int16), hf.bits, n + 16, out=np.zeros(n + 16, np.uint8))
+        X = np.zeros(n + 16 + nb + 4096, np.uint8)
+        X[n + 16: n + 16 + nb] = hf.payload
+        pay = X[n + 16: n + 16 + nb]                                        # inside out's range
+        for _ in range(2):
+            got = dec.decode_host(pay, hf.bits, X.size, out=X)
+            assert np.array_equal(got, ref)
+        Y = np.zeros(n + 64, np.uint8)                                      # the output moves
+        for _ in range(2):
+            got = dec.decode_host(pay, hf.bits, n + 16, out=Y)
+            assert np.array_equal(got, ref)
+        Z = np.zeros(n + 16 + nb, np.uint8)                                 # payload at out's tail,
+        Z[-nb:] = hf.payload                                                # past the cap given
+        got = dec.decode_host(Z[-nb:], hf.bits, n + 16, out=Z)
+        assert np.array_equal(got, ref)
+        dec.release_host()
+        got = dec.decode_host(pay, hf.bits, n + 16, out=Y)
+        assert np.array_equal(got, ref)
+    finally:
+        dec.close()
+
+
 @pytest.mark.parametrize("env", [{"HH_FRONT_WALK": "2"}, {"HH_FRONT_WALK": "16"},
                                  {"HH_FRONT_WALK": "8192"}, {"HH_EMIT_XPT": "0"},
                                  {"HH_EMIT_XPT": "1"}, {"HH_EMIT_NW": "8"}])

@@ -15,7 +15,7 @@ for round in $(seq ${ROUNDS:-2}); do
   for v in "${VARS[@]}"; do
     read -r lib envs <<< "$v"
     [ "$lib" = "-" ] && L=$GRAFT_REPO_ROOT/huffmandecoderongpus_amd/libhiphuff.so || L=$GRAFT_REPO_ROOT/build/var/$lib.so
-    r=$(env HIPHUFF_LIB=$L $envs timeout -k 10 180 python3 tools/time_lib.py ${MIB:-1024} 7 $SRC 2>>gpurun_out/ab.err) || { echo "[$v] failed"; exit 1; }
+    r=$(env HIPHUFF_LIB=$L HIPHUFF_AB_BUILD=1 $envs timeout -k 10 180 python3 tools/time_lib.py ${MIB:-1024} 7 $SRC 2>>gpurun_out/ab.err) || { echo "[$v] failed"; exit 1; }
     echo "[$v] $r"
   done
 done

@@ -80,59 +80,7 @@ res = {"lib": os.path.basename(os.environ.get("HIPHUFF_LIB", H.LIB_PATH)), "mib"
        "ok": bool(ok), "fast": dec.stats()["exact_fallback"] == 0}
 res.update({k: round(statistics.median(v), 4) for k, v in ph.items()})
 res["wall_ms"] = round(statistics.median(wall[1:]), 3)
-if os.environ.get("HH_WSPAN"):             # a -DHH_WSPAN build: per-wave start / fill / end (100 MHz clock)
-    import ctypes as C
-    import numpy as np
-    N = 8192
-    buf = (C.c_uint64 * (16 + 10 * N))()
-    H.lib().hh_debug_counters(dec._h, buf)
-    a = np.ctypeslib.as_array(buf)[16:].astype(np.int64)
-    if os.environ.get("HH_WSPAN_DUMP"):
-        np.save(os.environ["HH_WSPAN_DUMP"] + f"_{mib}.npy", a)
-    for name, o in (("cnt", 0), ("emf", 3 * N)):
-        st = a[o:o + 3 * N].reshape(N, 3).copy()
-        st = st[st[:, 2] > 0]
-        if not len(st):
-            continue
-        ev = st[:, 1] >> 48                    # (events in the fill stamp's top bits: walk rounds, fixes << 10)
-        st[:, 1] &= (1 << 48) - 1
-        t0 = st[:, 0].min()
-        us = lambda x: np.round(np.asarray(x) / 100.0, 2).tolist()   # noqa: E731  (100 MHz ticks -> us)
-        dur = st[:, 2] - st[:, 0]
-        ends = np.sort(st[:, 2] - t0)
-        res[name + "_span"] = {"waves": int(len(st)), "kernel_us": us(ends[-1]),
-                               "start_spread_us": us(st[:, 0].max() - t0),
-                               "fill_us_mean": us((st[:, 1] - st[:, 0]).mean()),
-                               "wave_us_p0_p50_p90_p99_max": us(np.percentile(dur, [0, 50, 90, 99, 100])),
-                               "end_us_p1_p10_p50_p90_max": us(np.percentile(ends, [1, 10, 50, 90, 100]))}
-        if name == "cnt":                      # (k_cntm's per-wave phase ticks: heads, counts, walks, the rest)
-            ph = a[6 * N:10 * N].reshape(N, 4)[np.nonzero(a[2:3 * N:3] > 0)[0]]
-            tot = ph.sum(axis=1).clip(min=1)
-            res[name + "_span"]["phase_frac_heads_counts_walks_rest"] = np.round(ph.sum(axis=0) / tot.sum(), 4).tolist()
-        if ev.any():
-            rounds, fixes = ev & 1023, ev >> 10
-            slow = np.argsort(st[:, 2] - st[:, 0])[-20:]
-            res[name + "_span"].update({"walk_rounds_total": int(rounds.sum()), "walk_rounds_p50_p99_max":
-                                        np.percentile(rounds, [50, 99, 100]).tolist(), "fixes_total": int(fixes.sum()),
-                                        "slowest20_rounds": rounds[slow].tolist(), "slowest20_fixes": fixes[slow].tolist()})
-elif os.environ.get("HH_DIAG") == "fsm":     # a -DHH_DIAG build: k_cnt phase cycles and walks
-    import ctypes as C
-    buf = (C.c_uint64 * 16)()
-    H.lib().hh_debug_counters(dec._h, buf)
-    cyc = [buf[i] for i in range(4)]
-    tot = sum(cyc) or 1
-    res["cnt_phase_frac"] = {n: round(cyc[i] / tot, 3) for n, i in
-                             (("head", 0), ("count", 1), ("walks", 2), ("records", 3))}
-    res["cnt_tiles"] = buf[8]
-    res["cnt_walk_tiles"] = buf[9]
-    res["cnt_walk_rounds"] = buf[10]
-    res["cnt_cycles_per_tile"] = round(tot / max(buf[8], 1), 1)
-    ecyc = [buf[i] for i in range(4, 8)]
-    etot = sum(ecyc) or 1
-    res["emf_phase_frac"] = {n: round(ecyc[i] / etot, 3) for n, i in
-                             (("prologue", 0), ("region", 1), ("edges", 2), ("copyout", 3))}
-    res["emf_cycles_per_tile"] = round(etot / max(buf[8], 1), 1)
-elif os.environ.get("HH_DIAG"):            # a -DHH_DIAG build: phase cycles and walk lengths
+if os.environ.get("HH_DIAG"):              # a -DHH_DIAG build (round 2 pipeline): phase cycles and walk lengths
     import ctypes as C
     buf = (C.c_uint64 * 16)()
     H.lib().hh_debug_counters(dec._h, buf)
