@@ -178,9 +178,10 @@ def cpu_baseline_tiled(H, hf, text, mib: int, jumpbits: int, reps: int, procs: i
 
 
 def phase_split(device: int, tree, flags: int, data, bits: int, out, n: int = 3) -> dict:
-    """Count / scan / emission device times from a separate decoder with
-    HH_FLAG_PHASE_TIMING (events between the kernels, ~6 us of idle GPU
-    each: never in the timed decodes), after the timed region."""
+    """Count / scan / emission device times of the TWO-PASS form, from a
+    separate decoder with HH_FLAG_PHASE_TIMING (events between its kernels,
+    ~6 us of idle GPU each: never in the timed decodes), after the timed
+    region.  (The single pass is one kernel: no split.)"""
     import torch
     import huffmandecoderongpus_amd as H
     d = H.Decoder(device, flags=flags | H.FLAG_PHASE_TIMING)
@@ -232,7 +233,8 @@ def device_workload(name: str, dec, data, bits: int, out, n_want: int, verify, s
             "roofline_frac": round(ach / HBM_PEAK_GBS, 4),
             "fast_path": all(s["exact_fallback"] == 0 for s in st),
             "fixed_length_path": all(s["fixed_length"] == 1 for s in st),
-            "state_machine_path": all(s["state_machine"] == 1 for s in st)}
+            "state_machine_path": all(s["state_machine"] in (1, 2) for s in st),
+            "single_pass": all(s["state_machine"] == 2 for s in st)}
 
 
 def gpu_local_cpus(device: int = 0):
@@ -525,7 +527,8 @@ def main():
     phases = (phase_split(local, syn.tree, 0, syn.data, syn.bits, out) if world == 1
               else {"sync": None, "scan": None, "emit": None})
     fast = all(s["exact_fallback"] == 0 for s in dev_ms)
-    kernels = ("k_cntm+k_fscan1+k_emf" if all(s["state_machine"] for s in dev_ms)
+    kernels = ("k_one" if all(s["state_machine"] == 2 for s in dev_ms)
+               else "k_cntm+k_fscan1+k_emf" if all(s["state_machine"] for s in dev_ms)
                else "k_front+k_walk+k_table+k_scan1+k_scan2+k_emit")
     extra = {}
     if world > 1:
@@ -584,12 +587,13 @@ def main():
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "bytes_alg": C_bytes + D_bytes, "ms_kernel": round(ms_dev, 4),
-                     "ms_front": phases["sync"], "ms_scan": phases["scan"],
-                     "ms_emit": phases["emit"]},
+                     "two_pass_split_ms": {"count": phases["sync"], "scan": phases["scan"],
+                                           "emit": phases["emit"]}},
         "decoded_MBps_device": round(D_bytes / (ms_dev * 1e-3) / 1e6, 1),
         "ms_per_call_sync": round(sync_ms, 4) if sync_ms is not None else None,
         "fast_path": fast,
-        "state_machine_path": all(s["state_machine"] == 1 for s in dev_ms),
+        "state_machine_path": all(s["state_machine"] in (1, 2) for s in dev_ms),
+        "single_pass": all(s["state_machine"] == 2 for s in dev_ms),
     }
     res.update(extra)
     if world == 1:

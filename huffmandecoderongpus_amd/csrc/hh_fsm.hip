@@ -1479,6 +1479,14 @@ static int fsm_grids(FsmDev *fd) {
     if (!kc || !ke) return HH_ERR_UNSUPPORTED;
     int pc = 0, pe = 0, ncu = 0, dev = 0;
     FS_OK(hipGetDevice(&dev));
+    // the table lookups address LDS from 0 (hh_fsm_kern.h): the kernels may
+    // declare no static LDS
+    const void *kst[3] = {(const void *)kc, (const void *)ke,
+                          (const void *)(fd->cm > 1 ? kcntm_for(sw, fd->cb, fd->cm) : nullptr)};
+    for (const void *k : kst) {
+        hipFuncAttributes fa;
+        if (k && (hipFuncGetAttributes(&fa, k) != hipSuccess || fa.sharedSizeBytes != 0)) return HH_ERR_INTERNAL;
+    }
     FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kc, 64 * CW, lds_cnt(fd)));
     FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, ke, 64 * emf_waves(), lds_emf(fd)));
     FS_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));

@@ -357,11 +357,30 @@ __device__ __forceinline__ OneLB one_lookback(uint64_t *st, uint32_t t, uint32_t
 
 // One tile t (uniform) with its words w (region j's, lane j) and pv (the 16
 // bytes before the tile, uniform).  colb: the wave's column area.
-template <uint32_t SW, uint32_t K, bool TAIL, uint32_t COI>
+// The tile's guesses (decodeallbits' heads): gn, lane j's for region j+1
+// (over the last G bits of its own region), and g0, lane 0's for region 0
+// (over the 16 bytes before the tile), as emission-table rows.
+template <uint32_t SW, uint32_t K>
+__device__ __forceinline__ void one_heads(const OneGeo &geo, uint32_t t, const uint32_t *w, const uint32_t *pv, uint32_t &gn,
+                                          uint32_t &g0) {
+    constexpr uint32_t RSH = HH_FSM_ET_RSH(K), HS = one_hs(SW, K);
+    gn = geo.gs ? head_row<SW, K, HS>(w, geo.gs) : 0u;
+    g0 = t == 0 ? geo.in_state << RSH : (geo.gs ? head_row<4, K, HS>(pv, geo.gs) : 0u);
+}
+
+// One tile t (uniform) with its words w (region j's, lane j) and its
+// guesses (one_heads).  colb: the wave's column area.  between(): called
+// once the tile's look-back is done, before its output is staged and
+// copied out (the wave takes its next tile there and issues its loads: a
+// wave holds no ticket while it may wait -- a ticket taken a tile ahead,
+// by a wave then waiting in its look-back, held up the tile every later
+// look-back waited for, and the decode ran tile by tile).
+template <uint32_t SW, uint32_t K, bool TAIL, uint32_t COI, typename Between>
 __device__ __forceinline__ void one_tile(uint8_t *smem, const OneGeo &geo, const OneWork &wk, uint8_t *__restrict__ out,
-                                         uint64_t cap, uint32_t t, const uint32_t *w, const uint32_t *pv, uint32_t er_off,
-                                         const uint32_t *b1, const uint8_t *ts, uint32_t colb, OneDbg &dg) {
-    constexpr uint32_t S = 32 * SW, RSH = HH_FSM_ET_RSH(K), HS = one_hs(SW, K);
+                                         uint64_t cap, uint32_t t, const uint32_t *w, uint32_t gn, uint32_t g0,
+                                         uint32_t er_off, const uint32_t *b1, const uint8_t *ts, uint32_t colb, OneDbg &dg,
+                                         Between between) {
+    constexpr uint32_t S = 32 * SW, RSH = HH_FSM_ET_RSH(K);
     const bool don = ONE_DBG_ON(wk);
     uint64_t tdg = don ? __builtin_amdgcn_s_memtime() : 0;
     dg.inc(OD_TILES);
@@ -378,9 +397,7 @@ __device__ __forceinline__ void one_tile(uint8_t *smem, const OneGeo &geo, const
 #pragma unroll
     for (uint32_t k = 0; k < SW; k++) wv.v[k] = w[k];
 
-    // decodeallbits: the guesses, then the speculative emission
-    const uint32_t gn = geo.gs ? head_row<SW, K, HS>(w, geo.gs) : 0u;   // (for region j+1)
-    const uint32_t g0 = t == 0 ? geo.in_state << RSH : (geo.gs ? head_row<4, K, HS>(pv, geo.gs) : 0u);
+    // decodeallbits: the speculative emission from the guesses
     const uint32_t gup = shfl_up1(gn);
     uint32_t gr = j ? gup : g0;                       // the entry row of the lane's chain
     uint32_t n, x;
@@ -448,6 +465,7 @@ __device__ __forceinline__ void one_tile(uint8_t *smem, const OneGeo &geo, const
         }
     }
     if (j == 0) __hip_atomic_store(&stp[t], st_make(geo.epoch, fail ? 3u : 2u, 0u, x63, B + T), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    between();
     if (j == 0 && t == geo.ntiles - 1) {
         wk.res[0] = fail || geo.test_retry ? (uint32_t)FF_RETRY : 0u;
         wk.res[2] = (uint32_t)(B + T);
@@ -478,7 +496,7 @@ __device__ __forceinline__ void one_tile(uint8_t *smem, const OneGeo &geo, const
     uint32_t v[CAPR];
 #pragma unroll
     for (uint32_t k = 0; k < CAPR; k++) v[k] = k < kmax ? *(lds_u32p)(uintptr_t)(base + 256u * k) : 0u;
-    WAVE_SYNC();
+    WAVE_SYNC();                                      // (every lane's column read before the staging writes)
     // the tile's output, contiguous from the column area's byte a0: lane j's
     // bytes at o = a0 + L.  A dword is stored by the run holding its last byte
     // (zeros where earlier runs' bytes go); a run ending inside a dword ORs
@@ -529,12 +547,13 @@ __device__ __forceinline__ void one_tile(uint8_t *smem, const OneGeo &geo, const
 }
 
 // The tiles in which the stream ends (at most two per decode), out of line.
+// (the stream's last tile: its wave takes its next ticket after it)
 template <uint32_t SW, uint32_t K, uint32_t COI>
 __device__ __noinline__ void one_tile_tail(uint8_t *smem, OneGeo geo, OneWork wk, uint8_t *__restrict__ out, uint64_t cap,
-                                           uint32_t t, Words<SW> w, Words<4> pv, uint32_t er_off,
+                                           uint32_t t, Words<SW> w, uint32_t gn, uint32_t g0, uint32_t er_off,
                                            const uint32_t *b1, const uint8_t *ts, uint32_t colb) {
     OneDbg dg = {};
-    one_tile<SW, K, true, COI>(smem, geo, wk, out, cap, t, w.v, pv.v, er_off, b1, ts, colb, dg);
+    one_tile<SW, K, true, COI>(smem, geo, wk, out, cap, t, w.v, gn, g0, er_off, b1, ts, colb, dg, [] {});
 }
 
 // k_one: the whole decode of tiles [0, ntiles).  Workgroups of nw waves (the
@@ -612,27 +631,33 @@ __global__ __launch_bounds__(64 * ONE_WMAX) void k_one(const uint32_t *__restric
         const uint64_t pa = tw >= 4 ? tw - 4 : 0u;   // (tile 0: unused)
         ppv = __builtin_amdgcn_raw_buffer_load_b32(fs_rsrc(g, pa, geo.nwords), (int)(4u * (lane_id() & 3u)), 0, 0);
     };
+    // the tile loop: a tile's heads once its words are in, its emission and
+    // look-back, then (between) the next ticket and its loads, then this
+    // tile's output while they are in flight
     uint32_t t = take();
     prefetch(t);
     while (t != ONE_NONE) {
-        uint32_t w[SW], pv[4];
+        uint32_t w[SW], pv[4], gn, g0;
 #pragma unroll
         for (uint32_t k = 0; k < SW; k++) w[k] = pw[k];
 #pragma unroll
         for (uint32_t i = 0; i < 4; i++) pv[i] = (uint32_t)__builtin_amdgcn_readlane((int)ppv, i);
-        uint64_t tk = don ? __builtin_amdgcn_s_memtime() : 0;
-        const uint32_t tn = take();
-        prefetch(tn);
-        dg.stamp(don, OD_CYC_TAKE, tk);
-        if (t < geo.ne) one_tile<SW, K, false, COI>(smem, geo, wk, out, cap, t, w, pv, er_off, s_b1, s_ts, colb, dg);
-        else {
+        one_heads<SW, K>(geo, t, w, pv, gn, g0);
+        uint32_t tn = ONE_NONE;
+        auto between = [&] {
+            uint64_t tk = don ? __builtin_amdgcn_s_memtime() : 0;
+            tn = take();
+            prefetch(tn);
+            dg.stamp(don, OD_CYC_TAKE, tk);
+        };
+        if (t < geo.ne) {
+            one_tile<SW, K, false, COI>(smem, geo, wk, out, cap, t, w, gn, g0, er_off, s_b1, s_ts, colb, dg, between);
+        } else {
             Words<SW> ww;
-            Words<4> pp;
 #pragma unroll
             for (uint32_t k = 0; k < SW; k++) ww.v[k] = w[k];
-#pragma unroll
-            for (uint32_t i = 0; i < 4; i++) pp.v[i] = pv[i];
-            one_tile_tail<SW, K, COI>(smem, geo, wk, out, cap, t, ww, pp, er_off, s_b1, s_ts, colb);
+            one_tile_tail<SW, K, COI>(smem, geo, wk, out, cap, t, ww, gn, g0, er_off, s_b1, s_ts, colb);
+            between();
         }
         t = tn;
     }
@@ -744,6 +769,8 @@ int one_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
         FS_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pe, kf, 64 * fd->one_nw, fd->one_lds));
         FS_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
         if (pe < 1) return HH_ERR_UNSUPPORTED;
+        hipFuncAttributes fa;                        // (no static LDS: hh_fsm_kern.h)
+        if (hipFuncGetAttributes(&fa, (const void *)kf) != hipSuccess || fa.sharedSizeBytes != 0) return HH_ERR_INTERNAL;
         fd->one_grid = (uint32_t)(pe * ncu);
     }
     int rc = one_status(ws, nt, st);

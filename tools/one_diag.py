@@ -29,7 +29,7 @@ text = d0.decode_host(hf0.payload, hf0.bits, hf0.uncompressedsize + 3)
 d0.close()
 syn = synth.tiled_stream(hf0, text, mib << 20)
 out = torch.empty(syn.decoded_bytes + 4096, dtype=torch.uint8, device="cuda")
-dec = H.Decoder(0)
+dec = H.Decoder(0, lane_bits=int(os.environ.get("HH_LANE_BITS", "0")))
 dec.set_tree(syn.tree)
 buf = np.zeros(16, np.uint64)
 for i in range(3):
