@@ -8,11 +8,8 @@ rm -rf $D; mkdir -p $D/csrc $D/include
 for f in $(git ls-tree --name-only $REV huffmandecoderongpus_amd/csrc/); do git show $REV:$f > $D/csrc/$(basename $f); done
 for f in $(git ls-tree --name-only $REV include/); do git show $REV:$f > $D/include/$(basename $f); done
 F="-O3 -fPIC -std=c++17 --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value -Wno-comment -I$D/include -I$D/csrc"
-/opt/rocm/bin/hipcc $F -c $D/csrc/hh_device.hip -o $D/hh_device.o &
-/opt/rocm/bin/hipcc $F -c $D/csrc/hh_fsm.hip -o $D/hh_fsm.o &
-gcc -O3 -fPIC -std=gnu11 -I$D/include -I$D/csrc -c $D/csrc/hh_huff.c -o $D/hh_huff.o &
-gcc -O3 -fPIC -std=gnu11 -I$D/include -I$D/csrc -c $D/csrc/hh_plugin.c -o $D/hh_plugin.o &
-[ -f $D/csrc/hh_encode.hip ] && /opt/rocm/bin/hipcc $F -c $D/csrc/hh_encode.hip -o $D/hh_encode.o &
+for f in $D/csrc/*.hip; do /opt/rocm/bin/hipcc $F -c $f -o $D/$(basename $f .hip).o & done
+for f in $D/csrc/*.c; do gcc -O3 -fPIC -std=gnu11 -I$D/include -I$D/csrc -c $f -o $D/$(basename $f .c).o & done
 wait
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o build/var/$N.so $D/*.o
 rm -rf $D

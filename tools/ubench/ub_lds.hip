@@ -8,6 +8,13 @@
 // Prints, per configuration, the time, the wave-level lookups per CU per
 // cycle (at the measured clock-free ns: lookups per ns per CU) and the
 // chip-wide lookups per second.
+//
+// Entry geometries of the count step (one configuration
+// per run, `ub_lds rounds wpc ent`, for rocprofv3 --pmc SQ_INSTS_LDS
+// SQ_LDS_BANK_CONFLICT): ent 2 = the count table (u16, row-major: the bank
+// is bits 1..6 of the step's byte, whatever the state), ent 4 = u32 entries
+// row-major (84 KB), ent 3 = u16 entries state-interleaved (entry (s, b) at
+// (b x NS + s) x 2: the bank depends on the state as well as the byte).
 // Build: hipcc -O3 --offload-arch=gfx950 -o build/ub_lds tools/ubench/ub_lds.hip
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -27,13 +34,13 @@ __device__ __forceinline__ uint32_t mix(uint32_t x) {
 template <int ENT, int CH>
 __global__ void k_chain(const uint32_t *gt, uint32_t rounds, uint32_t *sink) {
     extern __shared__ __align__(16) uint8_t smem[];
-    constexpr uint32_t RB = ENT == 2 ? 512u : 1024u;
+    constexpr uint32_t RB = ENT == 2 || ENT == 3 ? 512u : 1024u;
     for (uint32_t i = threadIdx.x; i < NS * RB / 4; i += blockDim.x) ((uint32_t *)smem)[i] = gt[i];
     __syncthreads();
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t row[CH], acc = 0;
 #pragma unroll
-    for (int c = 0; c < CH; c++) row[c] = (mix(gid * 7 + c) % NS) * RB;
+    for (int c = 0; c < CH; c++) row[c] = (mix(gid * 7 + c) % NS) * (ENT == 3 ? 2u : RB);
     for (uint32_t r = 0; r < rounds; r++) {
         uint32_t w[CH][8];
 #pragma unroll
@@ -47,6 +54,19 @@ __global__ void k_chain(const uint32_t *gt, uint32_t rounds, uint32_t *sink) {
                 if (ENT == 2) {
                     const uint32_t b = __builtin_amdgcn_ubfe(w[c][k >> 2], 8 * (k & 3), 8) << 1;
                     const uint32_t e = *(const uint16_t __attribute__((address_space(3))) *)(uintptr_t)((row[c] & 0xfe00u) | b);
+                    row[c] = e;
+                    acc += e;
+                    asm volatile("" : "+v"(acc));
+                } else if (ENT == 4) {
+                    const uint32_t b = __builtin_amdgcn_ubfe(w[c][k >> 2], 8 * (k & 3), 8) << 2;
+                    const uint32_t e = *(const uint32_t __attribute__((address_space(3))) *)(uintptr_t)((row[c] & 0xfc00u) | b);
+                    row[c] = e;
+                    acc += e;
+                    asm volatile("" : "+v"(acc));
+                } else if (ENT == 3) {
+                    // row[c]: the state x 2; entry = next state x 2 | count << 12
+                    const uint32_t b = __builtin_amdgcn_ubfe(w[c][k >> 2], 8 * (k & 3), 8);
+                    const uint32_t e = *(const uint16_t __attribute__((address_space(3))) *)(uintptr_t)(b * (2u * NS) + (row[c] & 0xffeu));
                     row[c] = e;
                     acc += e;
                     asm volatile("" : "+v"(acc));
@@ -71,6 +91,11 @@ static void fill(uint32_t *h, int ent) {
     if (ent == 2) {
         uint16_t *t = (uint16_t *)h;
         for (int i = 0; i < NS * 256; i++) t[i] = (uint16_t)(((rand() % NS) << 9) | (rand() % 4));
+    } else if (ent == 3) {
+        uint16_t *t = (uint16_t *)h;
+        for (int i = 0; i < NS * 256; i++) t[i] = (uint16_t)(((rand() % NS) << 1) | (rand() % 4) << 12);
+    } else if (ent == 4) {
+        for (int i = 0; i < NS * 256; i++) h[i] = (uint32_t)(((rand() % NS) << 10) | (rand() % 4));
     } else {
         uint64_t *t = (uint64_t *)h;
         for (int i = 0; i < NS * 128; i++)
@@ -81,7 +106,7 @@ static void fill(uint32_t *h, int ent) {
 template <int ENT, int CH>
 static void run(int ncu, const uint32_t *gt, uint32_t *sink, int wpc, uint32_t rounds) {
     const int tb = 64 * (wpc < 16 ? wpc : 16), wgs = wpc / (tb / 64);
-    const size_t lds = NS * (ENT == 2 ? 512 : 1024);
+    const size_t lds = NS * (ENT == 2 || ENT == 3 ? 512 : 1024);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -109,8 +134,10 @@ int main(int argc, char **argv) {
     if (argc > 2) {           // one configuration: rounds wpc ent (2 | 8), one chain per lane
         const int wpc = atoi(argv[2]), ent = argc > 3 ? atoi(argv[3]) : 2;
         fill(h, ent);
-        CK(hipMemcpy(gt, h, NS * (ent == 2 ? 512 : 1024), hipMemcpyHostToDevice));
+        CK(hipMemcpy(gt, h, NS * (ent == 2 || ent == 3 ? 512 : 1024), hipMemcpyHostToDevice));
         if (ent == 2) run<2, 1>(ncu, gt, sink, wpc, rounds);
+        else if (ent == 3) run<3, 1>(ncu, gt, sink, wpc, rounds);
+        else if (ent == 4) run<4, 1>(ncu, gt, sink, wpc, rounds);
         else run<8, 1>(ncu, gt, sink, wpc, rounds);
         return 0;
     }
