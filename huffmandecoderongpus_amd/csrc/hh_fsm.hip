@@ -1510,7 +1510,7 @@ static int fsm_grids(FsmDev *fd) {
     return HH_OK;
 }
 
-static int ws_need(FsmWs *ws, size_t need) {
+static int ws_need(FsmWs *ws, size_t need, hipStream_t st) {
     if (ws->size >= need) return HH_OK;
     if (ws->p) {
         FS_OK(hipDeviceSynchronize());   // (an asynchronous decode may still use it)
@@ -1521,7 +1521,11 @@ static int ws_need(FsmWs *ws, size_t need) {
     const size_t sz = need + need / 8;
     if (hipMalloc(&ws->p, sz) != hipSuccess) return HH_ERR_NOMEM;
     ws->size = sz;
-    FS_OK(hipMemset(ws->p, 0, 64));   // the status word and the scan's block ticket (the scan's last block clears it)
+    // the status word and the scan's block ticket (the scan's last block
+    // clears it), zeroed on the decode's stream: a plain hipMemset goes to
+    // the null stream, which a non-blocking decode stream does not wait
+    // for -- it could land while the first decode's scan counts its tickets
+    FS_OK(hipMemsetAsync(ws->p, 0, 64, st));
     return HH_OK;
 }
 
@@ -1582,7 +1586,7 @@ int fsm_launch(FsmDev *fd, FsmWs *ws, uint32_t slot, hipEvent_t *ev, const void 
     const size_t o_lex = o_fx + (nt + 1) * FX_W * 4, o_fxs = o_lex + (nt + 1) * 4;
     const size_t o_blk = (o_fxs + (nt + 1) * 4 + 7) & ~(size_t)7;
     const size_t o_bmax = o_blk + (size_t)nblk * 8;
-    rc = ws_need(ws, o_bmax + (size_t)nblk * 4);
+    rc = ws_need(ws, o_bmax + (size_t)nblk * 4, st);
     if (rc) return rc;
     uint8_t *w = (uint8_t *)ws->p;
     FsmWork wk;

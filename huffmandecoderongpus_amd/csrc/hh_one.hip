@@ -705,6 +705,7 @@ void one_setup(FsmDev *fd, uint32_t G, double avg, uint32_t minlen) {
     uint32_t capd = (uint32_t)(est * 1.25 / 4.0) + 2u;
     const uint32_t worst = (fd->S / (minlen ? minlen : 1u) + 1u + 3u) / 4u;
     if (capd > worst) capd = worst;
+    if (capd > ONE_CAPMAX) capd = ONE_CAPMAX;        // (short codes: regions past the columns go straight to HBM)
     if (getenv("HH_ONE_CAPD")) capd = (uint32_t)atoi(getenv("HH_ONE_CAPD"));   // (tests: forced overflows)
     if (capd < 2u || capd > ONE_CAPMAX) return;
     const uint32_t tabb = emf_tab_bytes(fd->ns, K, fd->r);

@@ -85,7 +85,9 @@ def test_single_pass_fixture(hh, files_dir, name):
 def test_single_pass_cut_random_trees(hh, nleaves, seed):
     """Random trees (up to 255 states: 224-bit regions, 5- or 6-bit steps)
     on i.i.d. streams cut mid-code (the tail rule) and at lengths that leave
-    a partial last tile, lanes past the end, or a single region."""
+    a partial last tile, lanes past the end, or a single region.  (3 and 12
+    leaves: codes so short that regions overflow the 128-B columns and go
+    straight to HBM, one_direct.)"""
     rng = np.random.default_rng(seed)
     iz, io, sy, syms = _random_tree(rng, nleaves)
     p = rng.dirichlet(np.full(nleaves, 0.5))
@@ -211,7 +213,7 @@ def test_single_pass_two_decoders_two_streams(hh, files_dir):
             d.set_tree(syn.tree)
         torch.cuda.synchronize()
         for _ in range(3):
-            ns = [d.decode_device_async(syn.data, syn.bits, o, s.cuda_stream) for d, o, s in zip(decs, outs, streams)]
+            ns = [d.decode_device_async(syn.data, syn.bits, o, s) for d, o, s in zip(decs, outs, streams)]
             for d in decs:
                 d.wait()
             torch.cuda.synchronize()
