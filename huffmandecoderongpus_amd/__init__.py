@@ -369,7 +369,11 @@ class Decoder:
         keep = bool(self.flags & FLAG_KEEP_HOST_PINNED)
         given = payload
         payload = np.ascontiguousarray(payload, np.uint8)
-        if keep and (out is None or payload is not given):
+        # (copied: the caller's memory is not what gets registered -- a new
+        # view of the same memory is fine, so the data pointers are compared)
+        copied = not (isinstance(given, np.ndarray)
+                      and given.__array_interface__["data"][0] == payload.__array_interface__["data"][0])
+        if keep and (out is None or copied):
             # the decoder keeps both buffers registered after the call: they
             # must be the caller's own arrays, alive until release_host()
             # (a temporary freed after the call could be reallocated at the
@@ -382,7 +386,7 @@ class Decoder:
         _check(lib().hh_decode_host(self._h, payload.ctypes.data, bits, out.ctypes.data, cap,
                                     C.byref(n)), "decode_host")
         if keep:
-            self._pinned = (payload, out)     # (alive while registered)
+            self._pinned = (given, out)       # (alive while registered)
         return out[: n.value]
 
     def release_host(self) -> None:

@@ -671,11 +671,12 @@ typedef void (*kone_t)(const uint32_t *, OneGeo, FsmTab, OneWork, uint8_t *, uin
 
 // (the region geometries of the state machine: 256-bit regions with 7-bit
 // steps for trees of <= 127 states, 224-bit regions with 5- or 6-bit steps
-// for larger ones; others keep the two-pass pipeline)
+// for larger ones, 4-bit steps for a tree with a 1-bit code; others keep the
+// two-pass pipeline)
 static kone_t kone_for(uint32_t sw, uint32_t K, uint32_t coi) {
 #define ONE_K(n, k) (coi <= 4 ? k_one<n, k, 4> : coi <= 6 ? k_one<n, k, 6> : k_one<n, k, 8>)
-    if (sw == 8) return K == 7 ? ONE_K(8, 7) : K == 6 ? ONE_K(8, 6) : K == 5 ? ONE_K(8, 5) : nullptr;
-    if (sw == 7) return K == 7 ? ONE_K(7, 7) : K == 6 ? ONE_K(7, 6) : K == 5 ? ONE_K(7, 5) : nullptr;
+    if (sw == 8) return K == 7 ? ONE_K(8, 7) : K == 6 ? ONE_K(8, 6) : K == 5 ? ONE_K(8, 5) : K == 4 ? ONE_K(8, 4) : nullptr;
+    if (sw == 7) return K == 7 ? ONE_K(7, 7) : K == 6 ? ONE_K(7, 6) : K == 5 ? ONE_K(7, 5) : K == 4 ? ONE_K(7, 4) : nullptr;
 #undef ONE_K
     return nullptr;
 }

@@ -94,10 +94,14 @@ def test_single_pass_cut_random_trees(hh, nleaves, seed):
     t = hh.Tree(iz, io, sy)
     text = rng.choice(syms, size=400_000, p=p).astype(np.uint8)
     data, bits = t.encode(text)
-    dec = hh.Decoder(0)
+    # (k_one is built for 256- and 224-bit regions: the smaller trees, whose
+    # default regions are shorter, are decoded with 256-bit ones; trees of
+    # more than 127 states take 224 bits by themselves)
+    dec = hh.Decoder(0, lane_bits=256 if nleaves <= 128 else 0)
     try:
         dec.set_tree(t)
         tb = dec.tile_bits()
+        assert tb in (64 * 256, 64 * 224), tb
         cuts = sorted({bits, bits - 1, bits // 3 + 7, tb - 1, tb, tb + 1, 5 * tb + 333, 300, 17})
         for cut in cuts:
             if cut <= 0 or cut > bits:
