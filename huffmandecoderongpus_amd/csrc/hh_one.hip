@@ -438,14 +438,7 @@ __device__ __forceinline__ void one_tile(uint8_t *smem, const OneGeo &geo, const
     uint32_t E = g0 >> RSH;
     uint64_t B = 0;
     uint64_t *stp = wk.st;
-#ifdef HH_ONE_XP_NOLB
-    // (timing experiment, never the product: no look-back, tile t's output
-    // placed at t x HH_ONE_XP_NOLB bytes -- the output is not the stream's)
-    if (t > 0) B = (uint64_t)t * HH_ONE_XP_NOLB;
-    if (false) {
-#else
     if (t > 0) {
-#endif
         // (a tile whose fix rounds ran out publishes a failed inclusive word
         // at once: no later scan may take it for a valid aggregate)
         if (j == 0)
