@@ -152,6 +152,29 @@ def confirm(first: dict, redone: dict, gather, rank: int, world: int, rows_ref: 
     return not missing and [list(map(int, r)) for r in rows] == [list(map(int, r)) for r in rows_ref]
 
 
+def pipelined(steps: int, launch, settle_one, wait) -> list:
+    """Full steps, pipelined: step k's decode is enqueued (launch(k) returns
+    its handle, whose results are valid once the next launch has returned or
+    wait() has), then step k-1 is settled -- its entry exchange and any redo,
+    settle_one(handle) -> its rows -- while step k's decode runs.  Every step
+    gets its own decode, exchange and redo; only their overlap changes.
+    Returns every step's rows, in step order.  Collective when settle_one is."""
+    got, prev = [], None
+    for k in range(steps):
+        h = launch(k)
+        if prev is not None:
+            got.append(settle_one(prev))
+        prev = h
+    wait()
+    if prev is not None:
+        got.append(settle_one(prev))
+    return got
+
+
+def _rows_eq(a: list, b: list) -> bool:
+    return [list(map(int, r)) for r in a] == [list(map(int, r)) for r in b]
+
+
 def out_base(rows: list, rank: int) -> int:
     return int(sum(int(rows[r][4]) for r in range(rank)))
 
@@ -211,7 +234,11 @@ class ShardJob:
         minlen = int(min(v for v in synth.code_lengths(self.tree) if v > 0))
         self.cap = s.owned_bits // minlen + 4096
         self.out = torch.empty(self.cap, dtype=torch.uint8, device=self.dev)
-        self.stream = torch.cuda.current_stream(self.dev)
+        self.out2 = None                # (pipelined_steps: the other step's output)
+        # the shard decodes on a stream of their own: a collective over
+        # device tensors (RCCL) waits for the current stream's work, and the
+        # pipelined steps' exchange must not wait for the next decode
+        self.stream = torch.cuda.Stream(self.dev)
         self.compressed_bytes = (s.owned_bits + 7) // 8
         self.decoded_bytes = 0
         self.rows = None
@@ -248,16 +275,18 @@ class ShardJob:
         nt = s.ntiles - (s.prologue - prologue) if s.t1 > s.t0 else 0
         return self.syn.data.data_ptr() + skip // 8, s.bits_avail - skip, nt
 
-    def _decode(self, in_state: int, prologue: int) -> dict:
+    def _decode(self, in_state: int, prologue: int, out=None) -> dict:
         ptr, bits, nt = self._args(prologue)
-        r = self.dec.decode_range_ptr(ptr, bits, nt, in_state, self.out.data_ptr(), self.cap,
+        out = self.out if out is None else out
+        r = self.dec.decode_range_ptr(ptr, bits, nt, in_state, out.data_ptr(), self.cap,
                                       self.stream.cuda_stream, prologue=prologue)
         r["in_state"] = r["entry_state"]
         return r
 
-    def _launch(self, in_state: int, prologue: int):
+    def _launch(self, in_state: int, prologue: int, out=None):
         ptr, bits, nt = self._args(prologue)
-        return self.dec.decode_range_async_ptr(ptr, bits, nt, in_state, self.out.data_ptr(), self.cap,
+        out = self.out if out is None else out
+        return self.dec.decode_range_async_ptr(ptr, bits, nt, in_state, out.data_ptr(), self.cap,
                                                self.stream.cuda_stream, prologue=prologue)
 
     def _first(self, r: dict) -> dict:
@@ -285,6 +314,41 @@ class ShardJob:
         self.rows, self.redo_state = self.last_rows, self.last_redo
         self.decoded_bytes = n
         return n
+
+    def pipelined_steps(self, steps: int) -> bool:
+        """`steps` full steps of this rank's shard (bench.py's timed steps for
+        N > 1), pipelined (shard.pipelined): step k's decode, entered in the
+        guessed state, is queued on the shard's stream; step k-1's exchange
+        (settle: the 5-integer all-gather) and any redo run while it is in
+        flight.  Nothing is carried over between steps: each step's redo
+        state comes from its own exchange.  The steps alternate between two
+        output buffers (a redo never writes over the next step's output);
+        the last one's is self.out.  True when every step's rows equal the
+        checked step's.  Collective (every rank calls it)."""
+        import torch
+        if steps <= 0:
+            return True
+        if self.out2 is None:
+            self.out2 = torch.empty_like(self.out)
+
+        def buf(k):
+            return self.out if (steps - 1 - k) % 2 == 0 else self.out2
+
+        def launch(k):
+            b = buf(k)
+            return self._launch(self.guess, self.seg.prologue, b), b
+
+        def settle_one(h):
+            r, b = h
+            first = r.as_dict()
+            first["in_state"] = first["entry_state"]
+            _, rows, redo = check_settle(self._first(first), lambda st: self._decode(st, 0, b), self._gather,
+                                         self.rank, self.world)
+            self.last_redo = redo
+            return rows
+        got = pipelined(steps, launch, settle_one, self.dec.wait)
+        self.last_rows = got[-1]
+        return self.rows is not None and all(_rows_eq(r, self.rows) for r in got)
 
     def decode_step(self) -> None:
         """One timed decode of this rank's shard: the prologue decode and, when

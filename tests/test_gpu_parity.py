@@ -923,6 +923,10 @@ def _shard_rank(rank, world, port, mib, q, backend="gloo", probe=2):
         torch.cuda.synchronize()
         ok = ok and job.verify()             # (the timed steps' output)
         ok = ok and job.confirm()            # the exchange after them agrees
+        job.out.fill_(0)
+        ok = ok and job.pipelined_steps(3)   # bench's timed steps: decode, exchange, redo, pipelined
+        torch.cuda.synchronize()
+        ok = ok and job.verify()             # (the last pipelined step's output)
         rep = job.gather_report()            # the assembled stream (gloo: host tensors)
         ok = ok and rep["allgather"]["seams_ok"]
         q.put((rank, ok, job.decoded_bytes, job.seg.prologue, job.redo_state))
@@ -938,8 +942,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.parametrize("probe", [2, 0])
 def test_shard_job_two_ranks_one_gpu(probe):
     """bench.py's multi-GPU path (ShardJob: shard plan, prologue entry, the
-    checked step's settle exchange, timed steps queued asynchronously with
-    no collective, the exchange after them confirming the checked rows,
+    checked step's settle exchange, decode-only steps queued asynchronously
+    with no collective, the exchange after them confirming the checked rows,
+    the pipelined full steps (each with its own exchange and redo),
     per-rank verification against the tiled text, the all-gather assembly
     checked on rank 0) with two processes sharing GPU 0 over gloo (RCCL
     needs distinct GPUs).  probe 0: rank 1 has no prologue and enters in a

@@ -276,3 +276,81 @@ def test_gloo_timed_steps_without_exchange(world, probe):
         assert not any_redo and all(bad for _, bad, _ in got)   # nothing to leave out
     else:
         assert any_redo and not any(bad for _, bad, _ in got)
+
+
+def _pipe_worker(rank, world, port, probe, name, q):
+    import torch.distributed as dist
+    import torch
+    import huffmandecoderongpus_amd as H
+    from huffmandecoderongpus_amd import shard
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        hf = H.HuffFile.load(os.path.join(FILES, name + ".huff"))
+        tree = hf.tree()
+        L = _femu()
+        seg = shard.plan(hf.bits, 64 * FSM_S, world, rank, probe)
+
+        def gather(vals):
+            t = torch.tensor(vals, dtype=torch.int64)
+            allt = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(allt, t)
+            return [a.tolist() for a in allt]
+
+        def first_run():
+            r = femu_segment(L, tree, hf.payload, seg, 0, seg.prologue)
+            if seg.prologue == 0 and seg.t0 > 0:
+                r["entry_exact"] = False
+            return r
+
+        def redo(st):
+            return femu_segment(L, tree, hf.payload, seg, st, 0)
+        _, rows, redo_state = shard.check_settle(first_run(), redo, gather, rank, world)
+        log, redos = [], []
+
+        def launch(k):
+            log.append(("launch", k))
+            return k, first_run()
+
+        def settle_one(h):
+            k, first = h
+            log.append(("settle", k))
+            _, r, st = shard.check_settle(first, redo, gather, rank, world)
+            redos.append(st)
+            return r
+        got = shard.pipelined(3, launch, settle_one, lambda: log.append(("wait",)))
+        ok = len(got) == 3 and all(shard._rows_eq(g, rows) for g in got)
+        order = log == [("launch", 0), ("launch", 1), ("settle", 0), ("launch", 2), ("settle", 1), ("wait",),
+                        ("settle", 2)]
+        own = all(st == redo_state for st in redos)       # each step found the redo itself
+        flags = [None] * world
+        dist.all_gather_object(flags, (ok, order, own, redo_state is not None))
+        if rank == 0:
+            q.put(flags)
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put(repr(e))
+        raise
+
+
+@pytest.mark.skipif(not os.path.exists(EMU), reason="tests/emu/libhh_emu.so not built")
+@pytest.mark.parametrize("world,probe", [(2, 2), (4, 0)])
+def test_gloo_pipelined_full_steps(world, probe):
+    """bench.py's timed multi-GPU steps (shard.pipelined, ShardJob.
+    pipelined_steps) over gloo with the state-machine emulation: step k's
+    exchange and redo run after step k+1's decode is launched, every step
+    settles its own entries (probe 0: the redo of a guessed entry, found by
+    each step's own exchange) and ends with the checked step's rows."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_pipe_worker, args=(r, world, port, probe, "kjv.txt", q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = q.get(timeout=240)
+    for p in ps:
+        p.join(timeout=60)
+    assert not isinstance(got, str), got
+    assert all(ok and order and own for ok, order, own, _ in got)
+    assert any(r for _, _, _, r in got) == (probe == 0)
