@@ -287,6 +287,28 @@ def test_capacity_error_reports_the_total(hh, files_dir, chunk_kb, monkeypatch):
         dec.close()
 
 
+def test_first_decode_of_fresh_decoders_chunked(hh, files_dir, monkeypatch):
+    """The first decode of a new decoder allocates its workspace and zeroes
+    its scan ticket; that zeroing must be ordered before the decode's kernels
+    on the decoder's (non-blocking) stream.  Round 6's full GPU run caught a
+    null-stream hipMemset landing during the first decode's scan: chunked
+    hh_decode_host calls on fresh decoders returned 3/16 of the output.  Six
+    fresh decoders, each decoding kjv.txt in 512 KiB chunks as its first
+    call, every output checked against the reference's text hash."""
+    import hashlib
+    from huffmandecoderongpus_amd import synth
+    monkeypatch.setenv("HH_PIPE_CHUNK_KB", "512")
+    hf = hh.HuffFile.load(os.path.join(files_dir, "kjv.txt.huff"))
+    for _ in range(6):
+        dec = hh.Decoder(0)
+        try:
+            dec.set_tree(hf.tree())
+            out = dec.decode_host(hf.payload, hf.bits, hf.uncompressedsize + 3)
+        finally:
+            dec.close()
+        assert hashlib.sha256(out.tobytes()).hexdigest() == synth.KJV_SHA256
+
+
 @pytest.mark.parametrize("chunk_kb,mib", [(None, 1024), (4096, 64), (2, 1)])
 def test_evaluate_scope_pipeline(hh, files_dir, chunk_kb, mib, monkeypatch):
     """hh_decode_host (the reference's evaluate() scope) uploads the payload
