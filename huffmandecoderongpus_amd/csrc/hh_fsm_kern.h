@@ -46,9 +46,12 @@ __device__ __forceinline__ bool lds_base_is_zero(const void *smem) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)smem == 0u;
 }
 
-// A table into LDS at a workgroup's start: 16-B nontemporal loads, 8 of them
-// in flight per thread before their stores (a 42 or 85 KB table in one round
-// trip to L2; a loop of 4-B load -> store pairs waited for each load in turn).
+// A table into LDS at a workgroup's start: 16-B loads, 8 of them in flight
+// per thread before their stores (a 42 or 85 KB table in one round trip to
+// L2; a loop of 4-B load -> store pairs waited for each load in turn).
+// Plain loads: the table stays in each XCD's L2 for its other workgroups,
+// which all fill at once (round 6, same box: 64 MiB 0.0934-0.0953 ->
+// 0.0904-0.0914 ms against nontemporal loads, 1 GiB equal within noise).
 // bytes: a multiple of 16; dst and src 16-B aligned.
 __device__ __forceinline__ void lds_fill16(uint8_t *dst, const void *src, uint32_t bytes) {
     constexpr uint32_t UNR = 8;
@@ -59,7 +62,7 @@ __device__ __forceinline__ void lds_fill16(uint8_t *dst, const void *src, uint32
         u32x4 v[UNR];
 #pragma unroll
         for (uint32_t u = 0; u < UNR; u++)
-            if (i + u * step < n) v[u] = __builtin_nontemporal_load(s + i + u * step);
+            if (i + u * step < n) v[u] = s[i + u * step];
 #pragma unroll
         for (uint32_t u = 0; u < UNR; u++)
             if (i + u * step < n) d[i + u * step] = v[u];
